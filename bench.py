@@ -1,0 +1,205 @@
+#!/usr/bin/env python3
+"""Benchmark of the MI355X path-tracing hot path (BASELINE.json metric:
+"Mrays/sec + ms/frame @1920x1080, 8 bounces, 1/2/4/8 MI355X").
+
+Workload (N=1 default = config C2): the Cornell box (36 tris + the
+reference's metal sphere), 1920x1080, 8 bounces (loop i <= 8), frames 1..1024 with
+accumulate=0 on frame 1.  One *step* = one full progressive render of `spp` frames, issued
+as ceil(spp/chunk) fused launches, plus (N>1) the RCCL all-gather that assembles the
+row-interleaved image.  Inputs (scene, accumulator) are resident in HBM before timing.
+
+value = segments (ray-scene queries, computeShader.c:450) of all ranks / max-over-ranks
+wall time, in Mrays/s.  Segment counts come from an untimed counting pass of the same
+frames (reference traversal semantics, bit-identical image).
+
+Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--spp S] [--chunk C]
+       (N>1: python -m torch.distributed.run --nproc-per-node N bench.py --gpus N ...)
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+PKG = os.path.join(REPO, "opengl-path-tracing_amd")
+sys.path.insert(0, PKG)
+
+METRIC = "Mrays/sec + ms/frame @1920×1080, 8 bounces, 1/2/4/8 MI355X"
+HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+
+
+def algorithmic_bytes(cnt, pixels, first_launch_plain):
+    """40 B/node visit + 36 B/tri test + 16 B/sphere test + 52 B/hit,
+    plus 32 B per pixel per launch for the accumulator read+write (16 B when the launch
+    starts with accumulate=0 and so only writes)."""
+    b = 40 * cnt["node_visits"] + 36 * cnt["tri_tests"] + 16 * cnt["sphere_tests"] + 52 * cnt["hits"]
+    return b + pixels * (16 if first_launch_plain else 32)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--spp", type=int, default=1024)
+    ap.add_argument("--chunk", type=int, default=64, help="frames fused per kernel launch")
+    ap.add_argument("--width", type=int, default=1920)
+    ap.add_argument("--height", type=int, default=1080)
+    ap.add_argument("--bounces", type=int, default=8)
+    ap.add_argument("--scene", default="cornell", choices=["cornell", "bunny", "sponza"])
+    ap.add_argument("--variant", type=int, default=0)
+    ap.add_argument("--cpu-spp", type=int, default=1, help="spp of the bounded CPU-baseline sample")
+    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--traffic-json", default=os.path.join(REPO, "profiles", "traffic_latest.json"),
+                    help="PMC-derived HBM bytes per launch (written by tools/pmc_traffic.py)")
+    args = ap.parse_args()
+
+    import numpy as np
+    import torch
+
+    import pt_host
+    import pt_scenes
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    distributed = world > 1
+    if distributed:
+        import torch.distributed as dist
+        import pt_dist
+        torch.cuda.set_device(local_rank)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+
+    def barrier():
+        if distributed:
+            dist.barrier()
+
+    W, H, spp, chunk = args.width, args.height, args.spp, min(args.chunk, args.spp)
+    scene_dir = os.path.join(REPO, "scenes")
+    obj, mtl = pt_scenes.write_scene(args.scene, scene_dir) if rank == 0 or not distributed else (None, None)
+    barrier()
+    if obj is None:
+        obj = os.path.join(scene_dir, "%sobj.txt" % args.scene)
+        mtl = os.path.join(scene_dir, "%smtl.txt" % args.scene)
+    sb = pt_host.setupBuffers(obj, mtl)
+    pt = pt_host.PathTracer(W, H, max_bounce=args.bounces, display_mode=1, device=local_rank,
+                            rank=rank, world=world)
+    pt.set_kernel(args.variant)
+    pt.upload(sb)
+    launches = [(f0, min(chunk, spp - (f0 - 1))) for f0 in range(1, spp + 1, chunk)]
+
+    if distributed:
+        rmax = pt_dist.rows_max(H, world)
+        send = torch.zeros((rmax, W, 4), dtype=torch.float32, device="cuda")
+
+    def step():
+        for f0, n in launches:
+            pt.render_async(f0, n, 0 if f0 == 1 else 1)
+        pt.sync()
+        if distributed:
+            nbytes = pt.rows_local * W * 16
+            pt.copy_rows_device(send.data_ptr(), nbytes)
+            img = pt_dist.gather_image(send, H, world)
+            torch.cuda.synchronize()
+            return img
+        return None
+
+    for _ in range(args.warmup):
+        step()
+    pt.timing(reset=True)
+    barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    barrier()
+    dt = time.perf_counter() - t0
+    kern_ms, n_launch = pt.timing(reset=True)
+    if distributed:
+        t = torch.tensor([dt], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
+
+    # untimed counting pass over the same frames: exact reference-semantics work counts
+    pt.set_counting(True)
+    tot = dict(segments=0, node_visits=0, tri_tests=0, sphere_tests=0, hits=0)
+    alg_bytes = 0
+    for f0, n in launches:
+        pt.render(f0, n, 0 if f0 == 1 else 1)
+        _, cnt = pt.stats()
+        for k in tot:
+            tot[k] += cnt[k]
+        alg_bytes += algorithmic_bytes(cnt, pt.rows_local * W, f0 == 1)
+    pt.set_counting(False)
+    if distributed:
+        v = torch.tensor([tot["segments"], alg_bytes], dtype=torch.float64, device="cuda")
+        dist.all_reduce(v, op=dist.ReduceOp.SUM)
+        seg_all, bytes_all = float(v[0]), float(v[1])
+    else:
+        seg_all, bytes_all = float(tot["segments"]), float(alg_bytes)
+
+    ms_per_step = dt / args.steps * 1e3
+    value = seg_all * args.steps / dt / 1e6
+    avg_launch_ms = kern_ms / max(n_launch, 1)
+    bytes_per_launch = alg_bytes / len(launches)       # this rank's launches
+    achieved = bytes_per_launch / (avg_launch_ms * 1e-3) / 1e9
+
+    traffic = None
+    try:
+        with open(args.traffic_json) as fh:
+            tj = json.load(fh)
+        if tj.get("width") == W and tj.get("height") == H and tj.get("chunk") == chunk and tj.get("scene") == args.scene:
+            traffic = tj.get("hbm_bytes_per_launch")
+    except (OSError, ValueError):
+        pass
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        sys.path.insert(0, os.path.join(REPO, "tests"))
+        import oracle_lib
+        threads = min(args.cpu_threads, os.cpu_count() or 1)
+        t1 = time.perf_counter()
+        _, ccnt = oracle_lib.render(sb, W, H, max_bounce=args.bounces, n_frames=args.cpu_spp,
+                                    threads=threads, counters=True)
+        cdt = time.perf_counter() - t1
+        cpu = {"value": round(float(ccnt[0]) / cdt / 1e6, 3), "unit": "Mrays/s", "cores": threads,
+               "kind": "port",
+               "sample": "CPU restatement of computeShader.c semantics (oracle/pt_oracle.cpp, -O3, "
+                         "%d threads), same scene/camera/bounces at %dx%d, frames 1..%d (%d segments, %.2f s); "
+                         "ms/frame extrapolated = %.1f" % (threads, W, H, args.cpu_spp, int(ccnt[0]), cdt,
+                                                            cdt * 1e3 / args.cpu_spp)}
+
+    if rank == 0:
+        line = {
+            "metric": METRIC, "value": round(value, 3), "unit": "Mrays/s", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_per_step, 3),
+            "higher_is_better": True, "scaling": "strong",
+            "vs_baseline": None, "dtype": "f32", "data": "synthetic",
+            "config": {"workload": "C2: %s %dx%d, %d spp (frames 1..%d), %d bounces (i<=%d), AA+sky+sphere on"
+                       % (args.scene, W, H, spp, spp, args.bounces, args.bounces),
+                       "scene": args.scene, "width": W, "height": H, "spp": spp, "max_bounce": args.bounces,
+                       "frames_per_launch": chunk, "kernel_variant": args.variant,
+                       "parallelism": "row-interleaved image split x%d + RCCL all-gather" % world if world > 1
+                       else "single GPU"},
+            "ms_per_frame": round(ms_per_step / spp, 4),
+            "segments_per_step": int(seg_all),
+            "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+                         "basis": "algorithmic bytes (SURVEY.md §8(d)) per launch / avg launch time (HIP events, "
+                                  "%d launches); cache-resident scene so frac can exceed 1" % n_launch,
+                         "avg_launch_ms": round(avg_launch_ms, 3)},
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(line), flush=True)
+    pt.close()
+    if distributed:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,107 @@
+/* pt_api.h -- C ABI of the MI355X path-tracing hot path (HIP kernels for gfx950).
+ *
+ * Drop-in for the reference's GL compute-program interface:
+ *   ComputeShader("computeShader.c")                 shader_c.h:14-60          -> pt_create
+ *   SSBOs at bindings 4..8 (glMapBufferRange)        ogl_path_trace.h:383-529  -> pt_upload_scene
+ *   camera SSBO re-upload (glBufferData)             ogl_path_trace.h:322-326  -> pt_set_camera
+ *   setInt("frame"/"accumulate"/"displayMode"...)    ogl_path_trace.h:174-182  -> pt_render args
+ *   glDispatchCompute(W/10, H/10, 1)                 ogl_path_trace.h:183      -> pt_render
+ *   glMemoryBarrier + textured quad readback         ogl_path_trace.h:186-192  -> pt_read_rgba32f
+ *   ACESFilm fragment shader                         screenQuadFrag.c:12-33    -> pt_read_rgba8_aces
+ *
+ * No torch / C++ types cross this boundary.  Every call is synchronous w.r.t. the host
+ * unless named *_async.  A context is not thread-safe: one context per thread.
+ * Return 0 on success, a negative PT_E* code otherwise; pt_last_error() explains.
+ */
+#ifndef PT_API_H
+#define PT_API_H
+
+#include <stddef.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define PT_OK 0
+#define PT_E_ARG (-1)      /* bad argument / size */
+#define PT_E_IO (-2)       /* file could not be opened */
+#define PT_E_PARSE (-3)    /* OBJ/MTL line too long or malformed */
+#define PT_E_SCENE (-4)    /* scene violates a limit or layout assumption */
+#define PT_E_HIP (-5)      /* HIP runtime error (no device, OOM, launch failure) */
+#define PT_E_STATE (-6)    /* call out of order (e.g. render before upload) */
+
+/* Flags mirroring the shader's compile-time toggles (computeShader.c:77-82). */
+#define PT_FLAG_NO_AA 1          /* antiAlias = false */
+#define PT_FLAG_NO_SKY 2         /* EnvironmentEnabled = false */
+#define PT_FLAG_NO_SPHERES 4     /* render_spheres = false */
+#define PT_FLAG_NO_TRIANGLES 8   /* render_triangles = false */
+#define PT_FLAG_REF_DISPATCH 16  /* write only the 10x10-group footprint of
+                                    glDispatchCompute(W/10, H/10) (ogl_path_trace.h:183) */
+
+typedef struct pt_ctx pt_ctx;
+
+typedef struct {
+    int width, height;       /* framebuffer (TEXTURE_WIDTH/HEIGHT, ogl_path_trace.h:45-46) */
+    int max_bounce;          /* maxBounceCount; loop is i <= max_bounce (computeShader.c:74,447) */
+    int display_mode;        /* 1 shaded, 2 normals, 3 albedo, 4 distance (computeShader.c:454-481) */
+    int flags;               /* PT_FLAG_* */
+    int rays_per_pixel;      /* raysPerPixel (computeShader.c:507); 1 in the reference */
+    int device;              /* HIP device ordinal */
+    int rank, world;         /* image partition: this context owns rows y = rank + k*world */
+} pt_config;
+
+int pt_create(const pt_config* cfg, pt_ctx** out);
+void pt_destroy(pt_ctx* ctx);
+const char* pt_last_error(const pt_ctx* ctx);
+
+/* Scene upload in the reference's std140 layouts (see pt_scene.h).  The library validates
+ * links/indices and transposes to its device layouts. */
+int pt_upload_scene(pt_ctx* ctx, const float* tris, int n_tris, const float* bvh, int n_nodes,
+                    const float* mats, int n_mats, const float* spheres, int n_spheres);
+
+/* cam: 12 floats {position.xyzw, direction.xyzw, data.xyzw} (computeShader.c:50-55). */
+int pt_set_camera(pt_ctx* ctx, const float cam[12]);
+
+/* Equivalent to n_frames reference dispatches with frame = frame_first .. frame_first+n-1;
+ * only the first uses accumulate = accumulate_first, the rest accumulate = 1 (running
+ * mean, computeShader.c:548-551).  Bit-identical to n_frames separate calls. */
+int pt_render(pt_ctx* ctx, int frame_first, int n_frames, int accumulate_first);
+/* Same, enqueued on the context's stream without waiting (timing / overlap). */
+int pt_render_async(pt_ctx* ctx, int frame_first, int n_frames, int accumulate_first);
+int pt_sync(pt_ctx* ctx);
+
+/* Local rows owned by this context: rows y = rank + k*world, k < rows_local. */
+int pt_rows(const pt_ctx* ctx, int* rows_local, int* row0, int* row_stride);
+
+/* Copies the local accumulation rows (rows_local * width * 4 floats, local row 0 =
+ * image row `rank`, image row 0 = bottom). */
+int pt_read_rgba32f(pt_ctx* ctx, float* host_dst, size_t bytes);
+/* ACES-tonemapped RGBA8 of the local rows, computed on the device. */
+int pt_read_rgba8_aces(pt_ctx* ctx, unsigned char* host_dst, size_t bytes);
+/* Overwrites the local accumulation rows (resume from a checkpoint / seed a test). */
+int pt_write_rgba32f(pt_ctx* ctx, const float* host_src, size_t bytes);
+
+/* Device pointer + size of the local accumulation buffer (for RCCL gathers). */
+int pt_accum_device(pt_ctx* ctx, void** dev_ptr, size_t* bytes);
+/* Stream-ordered device-to-device copy of the local rows into caller device memory
+ * (e.g. an RCCL send buffer); returns after the copy completed. */
+int pt_copy_rows_device(pt_ctx* ctx, void* dst_dev, size_t bytes);
+/* The hipStream_t the context renders on (as void*). */
+int pt_stream(pt_ctx* ctx, void** stream);
+
+/* Statistics of the last pt_render*: kernel ms (HIP events on the render stream), and
+ * when counting is enabled the reference-semantics work counts:
+ * out[0] segments, [1] node visits, [2] triangle tests, [3] sphere tests, [4] hits. */
+int pt_set_counting(pt_ctx* ctx, int enable);
+int pt_stats(pt_ctx* ctx, double* kernel_ms, unsigned long long out[5]);
+/* Sum of render-kernel durations (HIP events on the render stream) and the number of
+ * launches since the last reset; reset != 0 clears both after reading. */
+int pt_timing(pt_ctx* ctx, double* total_kernel_ms, int* n_launches, int reset);
+
+/* Kernel variant selection (0 = default/fastest); see DESIGN.md §5 for the list. */
+int pt_set_kernel(pt_ctx* ctx, int variant);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* PT_API_H */

@@ -1,0 +1,126 @@
+// ptrace -- headless C++ host driver: the reference's main.cpp/run() without the window.
+//
+//   main.cpp:6-11, ogl_path_trace.h:71-216 (run), :367-530 (setupBuffers)
+// The reference ignores argv and hard-codes scene_data/freeobj.txt (absent from the repo,
+// SURVEY.md §0.1); this driver honours the README's intent (readme.md:8-9): the .obj and
+// .mtl come from the command line.  Frames f = 1..spp are rendered with accumulate = 0
+// on frame 1 (ogl_path_trace.h:160-204 after a reset), fused `chunk` frames per launch,
+// optionally row-split across several GPUs of this node (one context per device).
+//
+// Output: RGBA32F accumulation as PFM (row 0 = bottom, like the GL texture) and the
+// ACES-tonemapped RGBA8 view as binary PPM (screenQuadFrag.c).
+#include "../../include/pt_api.h"
+#include "../../include/pt_scene.h"
+
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <string>
+#include <vector>
+
+static void usage() {
+    std::fprintf(stderr,
+                 "usage: ptrace <scene.obj> <scene.mtl> [--width W] [--height H] [--spp S] [--chunk C]\n"
+                 "              [--bounces B] [--mode 1..4] [--gpus G] [--pfm out.pfm] [--ppm out.ppm]\n"
+                 "              [--camera px py pz dx dy dz]\n");
+}
+
+#define CHECK(expr, ctx)                                                              \
+    do {                                                                              \
+        int rc_ = (expr);                                                             \
+        if (rc_) {                                                                    \
+            std::fprintf(stderr, "%s failed (%d): %s\n", #expr, rc_, pt_last_error(ctx)); \
+            return 1;                                                                 \
+        }                                                                             \
+    } while (0)
+
+int main(int argc, char** argv) {
+    if (argc < 3) { usage(); return 2; }
+    const char* obj = argv[1];
+    const char* mtl = argv[2];
+    int W = 1000, H = 800, spp = 64, chunk = 16, bounces = 5, mode = 1, gpus = 1;   // ogl_path_trace.h:45-46
+    std::string pfm = "out.pfm", ppm = "out.ppm";
+    float cam[12] = {0, -6, 1, 0, 0, 1, 0, 0, 0, 0, 0, 0};                          // ogl_path_trace.h:53-54
+    for (int i = 3; i < argc; i++) {
+        std::string a = argv[i];
+        auto next = [&](void) -> const char* { if (i + 1 >= argc) { usage(); std::exit(2); } return argv[++i]; };
+        if (a == "--width") W = std::atoi(next());
+        else if (a == "--height") H = std::atoi(next());
+        else if (a == "--spp") spp = std::atoi(next());
+        else if (a == "--chunk") chunk = std::atoi(next());
+        else if (a == "--bounces") bounces = std::atoi(next());
+        else if (a == "--mode") mode = std::atoi(next());
+        else if (a == "--gpus") gpus = std::atoi(next());
+        else if (a == "--pfm") pfm = next();
+        else if (a == "--ppm") ppm = next();
+        else if (a == "--camera") { for (int k = 0; k < 6; k++) cam[k < 3 ? k : k + 1] = (float)std::atof(next()); }
+        else { usage(); return 2; }
+    }
+    if (spp < 1 || chunk < 1 || gpus < 1) { usage(); return 2; }
+
+    auto t0 = std::chrono::steady_clock::now();
+    pt_scene* sc = nullptr;
+    int rc = pt_scene_load_obj(obj, mtl, &sc);
+    if (!rc) rc = pt_scene_add_builtins(sc);
+    if (!rc) rc = pt_scene_build_bvh(sc);
+    if (rc) { std::fprintf(stderr, "scene: %s (%d)\n", pt_scene_last_error(sc), rc); pt_scene_free(sc); return 1; }
+    int cnt[5];
+    pt_scene_counts(sc, cnt);
+    std::vector<float> tris(16 * (size_t)cnt[0]), mats(16 * (size_t)cnt[1]), sph(8 * (size_t)cnt[2]), nodes(12 * (size_t)cnt[3]);
+    pt_scene_get_tris(sc, tris.data(), cnt[0]);
+    pt_scene_get_mats(sc, mats.data(), cnt[1]);
+    pt_scene_get_spheres(sc, sph.data(), cnt[2]);
+    pt_scene_get_nodes(sc, nodes.data(), cnt[3]);
+    pt_scene_free(sc);
+    double t_scene = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    std::printf("# of polygons: %d  # of materials: %d (+5 built-in)  # of spheres: %d  BVH nodes: %d  (%.3f s)\n",
+                cnt[0], cnt[4], cnt[2], cnt[3], t_scene);
+
+    std::vector<pt_ctx*> ctx(gpus, nullptr);
+    for (int g = 0; g < gpus; g++) {
+        pt_config cfg = {W, H, bounces, mode, 0, 1, g, g, gpus};
+        CHECK(pt_create(&cfg, &ctx[g]), ctx[g]);
+        CHECK(pt_upload_scene(ctx[g], tris.data(), cnt[0], nodes.data(), cnt[3], mats.data(), cnt[1], sph.data(), cnt[2]), ctx[g]);
+        CHECK(pt_set_camera(ctx[g], cam), ctx[g]);
+    }
+    auto t1 = std::chrono::steady_clock::now();
+    for (int f0 = 1; f0 <= spp; f0 += chunk) {
+        int n = std::min(chunk, spp - f0 + 1);
+        for (int g = 0; g < gpus; g++) CHECK(pt_render_async(ctx[g], f0, n, f0 == 1 ? 0 : 1), ctx[g]);
+    }
+    for (int g = 0; g < gpus; g++) CHECK(pt_sync(ctx[g]), ctx[g]);
+    double secs = std::chrono::duration<double>(std::chrono::steady_clock::now() - t1).count();
+
+    std::vector<float> img(4 * (size_t)W * H, 0.0f);
+    std::vector<unsigned char> rgba(4 * (size_t)W * H, 0);
+    for (int g = 0; g < gpus; g++) {
+        int rows = 0, r0 = 0, rs = 1;
+        pt_rows(ctx[g], &rows, &r0, &rs);
+        std::vector<float> part(4 * (size_t)rows * W);
+        std::vector<unsigned char> part8(4 * (size_t)rows * W);
+        CHECK(pt_read_rgba32f(ctx[g], part.data(), part.size() * 4), ctx[g]);
+        CHECK(pt_read_rgba8_aces(ctx[g], part8.data(), part8.size()), ctx[g]);
+        for (int k = 0; k < rows; k++) {
+            int y = r0 + k * rs;
+            std::memcpy(&img[4 * (size_t)y * W], &part[4 * (size_t)k * W], 16 * (size_t)W);
+            std::memcpy(&rgba[4 * (size_t)y * W], &part8[4 * (size_t)k * W], 4 * (size_t)W);
+        }
+        pt_destroy(ctx[g]);
+    }
+    std::printf("rendered %dx%d, %d spp, %d bounces on %d GPU(s): %.3f s, %.3f ms/frame\n", W, H, spp, bounces,
+                gpus, secs, secs * 1e3 / spp);
+
+    if (FILE* f = std::fopen(pfm.c_str(), "wb")) {       // PFM rows run bottom-to-top: no flip
+        std::fprintf(f, "PF\n%d %d\n-1.0\n", W, H);
+        for (size_t i = 0; i < (size_t)W * H; i++) std::fwrite(&img[4 * i], 4, 3, f);
+        std::fclose(f);
+    }
+    if (FILE* f = std::fopen(ppm.c_str(), "wb")) {       // PPM rows run top-to-bottom: flip
+        std::fprintf(f, "P6\n%d %d\n255\n", W, H);
+        for (int y = H - 1; y >= 0; y--)
+            for (int x = 0; x < W; x++) std::fwrite(&rgba[4 * ((size_t)y * W + x)], 1, 3, f);
+        std::fclose(f);
+    }
+    return 0;
+}

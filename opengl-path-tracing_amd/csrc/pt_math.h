@@ -1,0 +1,163 @@
+// pt_math.h -- binary32 arithmetic of the hot path, shared by host-side precompute and the
+// gfx950 kernels.  Every function here is pinned so that the HIP kernels,
+// the host precompute and the CPU oracle round every operation identically:
+//   * IEEE binary32, round to nearest even, no contraction (build with -ffp-contract=off),
+//     correctly rounded division and square root;
+//   * dot(a,b) = (a.x*b.x + a.y*b.y) + a.z*b.z ; cross per the GLSL spec;
+//   * normalize(v) = v * (1 / sqrt(dot(v,v))) ; mix(x,y,a) = x*(1-a) + y*a ;
+//   * log: fdlibm e_logf algorithm; cos: Cephes cosf algorithm (octant reduction, 3-part pi/4).
+// computeShader.c leaves transcendental precision to the GL driver (implementation-defined);
+// these are the build's pinned choices (both < 2 ulp on the ranges the hot path feeds).
+#pragma once
+
+#include <stdint.h>
+
+#if defined(__HIPCC__)
+#include <hip/hip_runtime.h>
+#define PT_HD __host__ __device__ __forceinline__
+#else
+#include <math.h>
+#include <string.h>
+#define PT_HD inline
+#endif
+
+namespace pt {
+
+PT_HD uint32_t fbits(float f) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    return __float_as_uint(f);
+#else
+    uint32_t u; memcpy(&u, &f, 4); return u;
+#endif
+}
+PT_HD float bitsf(uint32_t u) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    return __uint_as_float(u);
+#else
+    float f; memcpy(&f, &u, 4); return f;
+#endif
+}
+PT_HD float fsqrt(float x) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    return __builtin_sqrtf(x);      // correctly rounded (-fhip-fp32-correctly-rounded-divide-sqrt)
+#else
+    return sqrtf(x);
+#endif
+}
+
+// fdlibm e_logf (FreeBSD constants).  x in {0} U [2^-32, 1] on the hot path.
+PT_HD float logf_pinned(float x) {
+    const float ln2_hi = 6.9313812256e-01f, ln2_lo = 9.0580006145e-06f, two25 = 3.355443200e+07f;
+    const float Lg1 = bitsf(0x3f2aaaaau), Lg2 = bitsf(0x3ecccce1u), Lg3 = bitsf(0x3e91e9eeu),
+                Lg4 = bitsf(0x3e789e26u);
+    int32_t ix = (int32_t)fbits(x);
+    int32_t k = 0;
+    if (ix < 0x00800000) {
+        if ((ix & 0x7fffffff) == 0) return bitsf(0xff800000u);   // -inf
+        if (ix < 0) return bitsf(0x7fc00000u);                    // NaN
+        k -= 25; x *= two25; ix = (int32_t)fbits(x);
+    }
+    if (ix >= 0x7f800000) return x + x;
+    k += (ix >> 23) - 127;
+    ix &= 0x007fffff;
+    int32_t i = (ix + (0x95f64 << 3)) & 0x800000;
+    x = bitsf((uint32_t)(ix | (i ^ 0x3f800000)));
+    k += (i >> 23);
+    float f = x - 1.0f;
+    float dk;
+    if ((0x007fffff & (0x8000 + ix)) < 0xc000) {
+        if (f == 0.0f) {
+            if (k == 0) return 0.0f;
+            dk = (float)k;
+            return dk * ln2_hi + dk * ln2_lo;
+        }
+        float R = f * f * (0.5f - 0.33333333333333333f * f);
+        if (k == 0) return f - R;
+        dk = (float)k;
+        return dk * ln2_hi - ((R - dk * ln2_lo) - f);
+    }
+    float s = f / (2.0f + f);
+    dk = (float)k;
+    float z = s * s;
+    int32_t ii = ix - (0x6147a << 3);
+    float w = z * z;
+    int32_t j = (0x6b851 << 3) - ix;
+    float t1 = w * (Lg2 + w * Lg4);
+    float t2 = z * (Lg1 + w * Lg3);
+    ii |= j;
+    float R = t2 + t1;
+    if (ii > 0) {
+        float hfsq = 0.5f * f * f;
+        if (k == 0) return f - (hfsq - s * (hfsq + R));
+        return dk * ln2_hi - ((hfsq - (s * (hfsq + R) + dk * ln2_lo)) - f);
+    }
+    if (k == 0) return f - s * (f - R);
+    return dk * ln2_hi - ((s * (f - R) - dk * ln2_lo) - f);
+}
+
+// Cephes cosf; valid for finite |x| < 8192 (the hot path feeds [0, 2*pi]).
+PT_HD float cosf_pinned(float xx) {
+    uint32_t ax = fbits(xx) & 0x7fffffffu;
+    if (ax >= 0x7f800000u) return bitsf(0x7fc00000u);
+    const float DP1 = 0.78515625f, DP2 = 2.4187564849853515625e-4f, DP3 = 3.77489497744594108e-8f,
+                FOPI = 1.27323954473516f;
+    float x = bitsf(ax);
+    int j = (int)(FOPI * x);
+    float y = (float)j;
+    if (j & 1) { j += 1; y += 1.0f; }
+    j &= 7;
+    bool neg = false;
+    if (j > 3) { j -= 4; neg = !neg; }
+    if (j > 1) neg = !neg;
+    x = ((x - y * DP1) - y * DP2) - y * DP3;
+    float z = x * x;
+    float r;
+    if (j == 1 || j == 2) {
+        r = ((-1.9515295891E-4f * z + 8.3321608736E-3f) * z - 1.6666654611E-1f) * z * x + x;
+    } else {
+        r = ((2.443315711809948E-005f * z - 1.388731625493765E-003f) * z + 4.166664568298827E-002f) * z * z;
+        r -= 0.5f * z;
+        r += 1.0f;
+    }
+    return neg ? -r : r;
+}
+
+struct f3 { float x, y, z; };
+PT_HD f3 mk(float x, float y, float z) { f3 r; r.x = x; r.y = y; r.z = z; return r; }
+PT_HD f3 operator+(f3 a, f3 b) { return mk(a.x + b.x, a.y + b.y, a.z + b.z); }
+PT_HD f3 operator-(f3 a, f3 b) { return mk(a.x - b.x, a.y - b.y, a.z - b.z); }
+PT_HD f3 operator*(f3 a, f3 b) { return mk(a.x * b.x, a.y * b.y, a.z * b.z); }
+PT_HD f3 operator*(f3 a, float s) { return mk(a.x * s, a.y * s, a.z * s); }
+PT_HD f3 operator/(f3 a, float s) { return mk(a.x / s, a.y / s, a.z / s); }
+PT_HD float dot(f3 a, f3 b) { return (a.x * b.x + a.y * b.y) + a.z * b.z; }
+PT_HD f3 cross(f3 a, f3 b) { return mk(a.y * b.z - b.y * a.z, a.z * b.x - b.z * a.x, a.x * b.y - b.x * a.y); }
+PT_HD float length(f3 a) { return fsqrt(dot(a, a)); }
+PT_HD f3 normalize(f3 a) { float r = 1.0f / fsqrt(dot(a, a)); return a * r; }
+PT_HD f3 mix(f3 x, f3 y, float a) {
+    float oma = 1.0f - a;
+    return mk(x.x * oma + y.x * a, x.y * oma + y.y * a, x.z * oma + y.z * a);
+}
+
+// PCG-style hash RNG (computeShader.c:87-98): uint32 wraparound; value/2^32 in [0,1].
+PT_HD uint32_t next_random(uint32_t& s) {
+    s = s * 747796405u + 2891336453u;
+    uint32_t r = ((s >> ((s >> 28) + 4)) ^ s) * 277803737u;
+    return (r >> 22) ^ r;
+}
+PT_HD float random01(uint32_t& s) { return (float)next_random(s) * (1.0f / 4294967296.0f); }
+PT_HD float random_normal(uint32_t& s) {            // :115-120 (theta first, then rho)
+    float theta = (2.0f * 3.1415926f) * random01(s);
+    float rho = fsqrt(-2.0f * logf_pinned(random01(s)));
+    return rho * cosf_pinned(theta);
+}
+PT_HD f3 random_unit_vector(uint32_t& s) {          // :122-129, x, y, z order
+    float x = random_normal(s);
+    float y = random_normal(s);
+    float z = random_normal(s);
+    return normalize(mk(x, y, z));
+}
+PT_HD uint32_t seed(int x, int y, int frame) {      // :514-515, mod 2^32
+    return ((uint32_t)y * 831266u + (uint32_t)x * 923766u) + (uint32_t)frame * 719393u;
+}
+
+}  // namespace pt

@@ -1,0 +1,684 @@
+// pt_render.hip -- the path-tracing hot path on MI355X (gfx950) behind the pt_api.h C ABI.
+//
+// Replaces LearnOpenGL/computeShader.c (main :505-554, Trace :434-501,
+// calculateRayCollision :367-432, bvh_intersect :309-365, hit_triangle :274-307,
+// hit_sphere :209-226, RNG :87-129) and the GL plumbing that drives it
+// (ogl_path_trace.h:160-204, 367-530).  Results are bit-identical to the CPU oracle's
+// restatement of those semantics; every float op is pinned via pt_math.h
+// and -ffp-contract=off.
+//
+// Device layouts, built once at pt_upload_scene from the std140 records:
+//   node  32 B : {min.xyz, a}, {max.xyz, b}   internal: a = hit link (left child), b = miss
+//                                             leaf:     a = ~(slot<<1 | single), b = next
+//   tri   64 B : {v0.xyz, n.x}, {v1.xyz, n.y}, {v2.xyz, n.z}, {d0, matIdx, 0, 0}
+//                n = normalize(cross(v1-v0, v2-v0)) and d0 = -dot(n, v0) are the exact values
+//                hit_triangle recomputes per call; a leaf's triangles sit in slots 2k, 2k+1.
+//   mat   48 B : {color.rgb, smoothness}, {emission*strength, specProb}, {specular.rgb, 0}
+//   sphere 32 B: {c.xyz, r*r}, {matIdx, 0, 0, 0}
+#include "pt_math.h"
+#include "../../include/pt_api.h"
+
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+using pt::f3;
+using pt::mk;
+
+namespace {
+
+struct DevScene {
+    const float4* nodes;
+    const float4* tris;
+    const float4* mats;
+    const float4* spheres;
+    int n_nodes, n_spheres;
+};
+
+struct KParams {
+    DevScene sc;
+    float4* accum;                 // rows_local x W
+    float cam[12];                 // pos, fwd, right, up (per-dispatch constants)
+    int W, H, row0, row_stride, rows_local;
+    int x_limit, y_limit;          // PT_FLAG_REF_DISPATCH footprint
+    int frame_first, n_frames, acc_first;
+    int max_bounce, mode, flags, rpp;
+    unsigned long long* counters;  // [5] when counting
+    unsigned int* work_counter;    // persistent kernel pixel queue
+};
+
+struct Cnt {
+    uint32_t seg, nodes, tri, sph, hits;
+};
+
+// ------------------------------------------------------------------ intersection
+// bvh_intersect (computeShader.c:309-365): the exact division/compare chain; NaN compares
+// are false, which decides axis-parallel rays and zero-thickness boxes.
+__device__ __forceinline__ bool slab(float4 lo, float4 hi, f3 o, f3 d, float cur_t) {
+    float tmin = (lo.x - o.x) / d.x;
+    float tmax = (hi.x - o.x) / d.x;
+    if (tmin > tmax) { float q = tmin; tmin = tmax; tmax = q; }
+    float tymin = (lo.y - o.y) / d.y;
+    float tymax = (hi.y - o.y) / d.y;
+    if (tymin > tymax) { float q = tymin; tymin = tymax; tymax = q; }
+    if ((tmin > tymax) || (tymin > tmax)) return false;
+    if (tymin > tmin) tmin = tymin;
+    if (tymax < tmax) tmax = tymax;
+    float tzmin = (lo.z - o.z) / d.z;
+    float tzmax = (hi.z - o.z) / d.z;
+    if (tzmin > tzmax) { float q = tzmin; tzmin = tzmax; tzmax = q; }
+    if ((tmin > tzmax) || (tzmin > tmax)) return false;
+    if (tzmin > tmin) tmin = tzmin;
+    return !(tmin > cur_t);
+}
+
+// hit_triangle (computeShader.c:274-307) with the per-triangle normal and plane offset
+// precomputed (same ops, same bits).  Returns -1 for a miss.  `tbest` cull: a hit at
+// t >= tbest can never be selected by the leaf's 2-way choice (:411-428), and a culled
+// value behaves like a miss in that choice, so culling before the edge tests is exact.
+__device__ __forceinline__ float tri_hit(const float4* T, f3 o, f3 d, float tbest, f3& n) {
+    float4 q0 = T[0], q1 = T[1], q2 = T[2], q3 = T[3];
+    n = mk(q0.w, q1.w, q2.w);
+    float t = -(pt::dot(n, o) + q3.x) / pt::dot(n, d);
+    if (t < 0.0f) return -1.0f;
+    if (!(t < tbest)) return -1.0f;
+    f3 v0 = mk(q0.x, q0.y, q0.z), v1 = mk(q1.x, q1.y, q1.z), v2 = mk(q2.x, q2.y, q2.z);
+    f3 p = o + d * t;
+    if (!(pt::dot(n, pt::cross(v1 - v0, p - v0)) > 0.0f)) return -1.0f;
+    if (!(pt::dot(n, pt::cross(v2 - v1, p - v1)) > 0.0f)) return -1.0f;
+    if (!(pt::dot(n, pt::cross(v0 - v2, p - v2)) > 0.0f)) return -1.0f;
+    return t;
+}
+
+// calculateRayCollision (computeShader.c:367-432)
+template <bool COUNT>
+__device__ __forceinline__ bool collide(const KParams& p, f3 o, f3 d, f3& normal, f3& hitp,
+                                        int& mat, Cnt& c) {
+    float t = __builtin_huge_valf();
+    bool hit = false;
+    if (!(p.flags & PT_FLAG_NO_SPHERES)) {
+        for (int si = 0; si < p.sc.n_spheres; si++) {
+            float4 s0 = p.sc.spheres[2 * si];
+            f3 cc = mk(s0.x, s0.y, s0.z);
+            f3 oc = o - cc;
+            float a = pt::dot(d, d);
+            float half_b = pt::dot(oc, d);
+            float cq = pt::dot(oc, oc) - s0.w;
+            float disc = half_b * half_b - a * cq;
+            float ht = disc < 0.0f ? -1.0f : (-half_b - pt::fsqrt(disc)) / a;
+            if (COUNT) c.sph++;
+            if (ht > 0.0001f && ht < t) {
+                f3 pn = pt::normalize((o + d * ht) - cc);
+                if (pt::dot(pn, d) > 0.0f) pn = pn * -1.0f;
+                hit = true;
+                t = ht;
+                normal = pn;
+                hitp = o + d * ht;
+                mat = __float_as_int(p.sc.spheres[2 * si + 1].x);
+            }
+        }
+    }
+    if ((p.flags & PT_FLAG_NO_TRIANGLES) || p.sc.n_nodes <= 0) return hit;
+    int bi = 0;
+    for (int steps = 0; bi > -1 && steps < p.sc.n_nodes; steps++) {
+        float4 lo = p.sc.nodes[2 * bi], hi = p.sc.nodes[2 * bi + 1];
+        int a = __float_as_int(lo.w), b = __float_as_int(hi.w);
+        bool hb = slab(lo, hi, o, d, t);
+        if (COUNT) c.nodes++;
+        int next = (hb && a >= 0) ? a : b;
+        if (hb && a < 0) {
+            if (COUNT) c.tri += 2;
+            int code = ~a;
+            const float4* T0 = p.sc.tris + 8 * (code >> 1);
+            f3 n0, n1;
+            float h1 = tri_hit(T0, o, d, t, n0);
+            float h2 = (code & 1) ? h1 : tri_hit(T0 + 4, o, d, t, n1);
+            if (code & 1) n1 = n0;
+            if (h1 > 0.0001f && h1 < t && (h1 < h2 || h2 < 0.0001f)) {
+                if (pt::dot(n0, d) > 0.0f) n0 = n0 * -1.0f;
+                hit = true;
+                t = h1;
+                normal = n0;
+                hitp = o + d * h1;
+                mat = __float_as_int(T0[3].y);
+            } else if (h2 > 0.0001f && h2 < t) {
+                if (pt::dot(n1, d) > 0.0f) n1 = n1 * -1.0f;
+                hit = true;
+                t = h2;
+                normal = n1;
+                hitp = o + d * h2;
+                mat = __float_as_int(T0[(code & 1) ? 3 : 7].y);
+            }
+        }
+        bi = next;
+    }
+    return hit;
+}
+
+// Trace (computeShader.c:434-501)
+template <bool COUNT>
+__device__ f3 trace(const KParams& p, f3 o, f3 d, uint32_t& state, Cnt& c) {
+    f3 incoming = mk(0, 0, 0), ray_color = mk(1, 1, 1);
+    f3 normal = mk(0, 0, 0), hitp = mk(0, 0, 0);
+    int mat = 0;
+    for (int i = 0; i <= p.max_bounce; i++) {
+        bool hit = collide<COUNT>(p, o, d, normal, hitp, mat, c);
+        if (COUNT) { c.seg++; if (hit) c.hits++; }
+        if (hit && pt::length(ray_color) > 0.01f) {
+            if (p.mode == 2) return (normal + mk(1, 1, 1)) * 0.5f;
+            if (p.mode == 4) {
+                float s = pt::length(hitp - o);
+                float dist = 1.0f - pt::fsqrt(s + 1.0f) / (s + 1.0f);
+                float q = dist * dist;
+                return mk(q, q, q);
+            }
+            o = hitp;
+            f3 diffuse = pt::normalize(normal + pt::random_unit_vector(state));
+            float k = 2.0f * pt::dot(normal, d);
+            f3 specular = pt::normalize(d - normal * k);
+            float4 m0 = p.sc.mats[3 * mat], m1 = p.sc.mats[3 * mat + 1], m2 = p.sc.mats[3 * mat + 2];
+            if (p.mode == 3) return mk(m0.x, m0.y, m0.z);
+            float is_spec = (m1.w > pt::random01(state)) ? 1.0f : 0.0f;
+            d = pt::mix(diffuse, specular, m0.w * is_spec);
+            incoming = incoming + mk(m1.x, m1.y, m1.z) * ray_color;
+            ray_color = ray_color * pt::mix(mk(m0.x, m0.y, m0.z), mk(m2.x, m2.y, m2.z), is_spec);
+        } else {
+            f3 env = mk(0, 0, 0);
+            if (!(p.flags & PT_FLAG_NO_SKY)) {
+                f3 dir = pt::normalize(d);
+                float tt = 0.5f * (dir.z + 1.0f);
+                float omt = 1.0f - tt;
+                env = mk(omt * 1.0f + tt * 0.5f, omt * 1.0f + tt * 0.7f, omt * 1.0f + tt * 1.0f);
+            }
+            incoming = incoming + env * ray_color;
+            break;
+        }
+    }
+    return incoming;
+}
+
+// main (computeShader.c:505-546): one sample of pixel (x, y) at `frame`.
+template <bool COUNT>
+__device__ __forceinline__ f3 sample_pixel(const KParams& p, int x, int y, int frame, Cnt& c) {
+    uint32_t state = pt::seed(x, y, frame);
+    f3 pos = mk(p.cam[0], p.cam[1], p.cam[2]), fwd = mk(p.cam[3], p.cam[4], p.cam[5]);
+    f3 right = mk(p.cam[6], p.cam[7], p.cam[8]), up = mk(p.cam[9], p.cam[10], p.cam[11]);
+    f3 pixel = mk(0, 0, 0);
+    for (int r = 0; r < p.rpp; r++) {
+        float ax = 0.0f, ay = 0.0f;
+        if (!(p.flags & PT_FLAG_NO_AA)) {
+            ax = pt::random01(state);
+            ay = pt::random01(state);
+        }
+        float u = ((float)x + ax) / (float)p.W - 0.5f;
+        float v = ((float)y + ay) / (float)p.H - 0.5f;
+        f3 d = pt::normalize((fwd + right * u) + up * v);
+        pixel = pixel + trace<COUNT>(p, pos, d, state, c);
+    }
+    return pixel / (float)p.rpp;
+}
+
+// :548-551 running mean, per component, no contraction.
+__device__ __forceinline__ float4 accumulate(float4 prev, f3 rgb, int frame, bool acc) {
+    if (!acc) return make_float4(rgb.x, rgb.y, rgb.z, 1.0f);
+    float ff = (float)frame;
+    float w = (ff - 1.0f) / ff;
+    return make_float4(prev.x * w + rgb.x / ff, prev.y * w + rgb.y / ff, prev.z * w + rgb.z / ff,
+                       prev.w * w + 1.0f / ff);
+}
+
+__device__ __forceinline__ unsigned long long wave_sum(unsigned long long v) {
+    for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+    return v;
+}
+
+template <bool COUNT>
+__device__ __forceinline__ void flush_counters(const KParams& p, const Cnt& c) {
+    if (!COUNT) return;
+    unsigned long long v[5] = {c.seg, c.nodes, c.tri, c.sph, c.hits};
+    for (int i = 0; i < 5; i++) {
+        unsigned long long s = wave_sum(v[i]);
+        if ((threadIdx.x & 63) == 0) atomicAdd(&p.counters[i], s);
+    }
+}
+
+// Variant 0: one lane per pixel, all n_frames fused in registers (one accumulator
+// read + write per launch), 16x16-pixel workgroups of four 8x8 wave tiles.
+template <bool COUNT>
+__global__ __launch_bounds__(256) void k_render_tiled(KParams p) {
+    int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    int lx = blockIdx.x * 16 + (wave & 1) * 8 + (lane & 7);
+    int lrow = blockIdx.y * 16 + (wave >> 1) * 8 + (lane >> 3);
+    Cnt c = {0, 0, 0, 0, 0};
+    int y = p.row0 + lrow * p.row_stride;
+    bool active = lx < p.W && lrow < p.rows_local && lx < p.x_limit && y < p.y_limit;
+    if (active) {
+        size_t idx = (size_t)lrow * p.W + lx;
+        float4 acc = p.acc_first ? p.accum[idx] : make_float4(0, 0, 0, 0);
+        for (int k = 0; k < p.n_frames; k++) {
+            int f = p.frame_first + k;
+            f3 rgb = sample_pixel<COUNT>(p, lx, y, f, c);
+            acc = accumulate(acc, rgb, f, k > 0 || p.acc_first == 1);
+        }
+        p.accum[idx] = acc;
+    }
+    flush_counters<COUNT>(p, c);
+}
+
+// ACES film tonemap epilogue (screenQuadFrag.c:12-26) -> RGBA8, alpha 255.
+__global__ __launch_bounds__(256) void k_aces(const float4* __restrict__ src, uchar4* __restrict__ dst,
+                                              long long n) {
+    long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    float4 v = src[i];
+    float c[3] = {v.x, v.y, v.z};
+    unsigned char o[3];
+    for (int k = 0; k < 3; k++) {
+        float x = c[k];
+        float tm = (x * (2.51f * x + 0.03f)) / (x * (2.43f * x + 0.59f) + 0.14f);
+        tm = tm < 0.0f ? 0.0f : (tm > 1.0f ? 1.0f : tm);
+        if (!(tm == tm)) tm = 0.0f;
+        o[k] = (unsigned char)(int)(tm * 255.0f + 0.5f);
+    }
+    dst[i] = make_uchar4(o[0], o[1], o[2], 255);
+}
+
+}  // namespace
+
+// ===================================================================== host side
+struct pt_ctx {
+    pt_config cfg{};
+    int rows_local = 0;
+    hipStream_t stream = nullptr;
+    std::vector<hipEvent_t> ev_free;                               // recycled events
+    std::vector<std::pair<hipEvent_t, hipEvent_t>> ev_pending;     // launches not yet synced
+    double total_ms = 0.0;
+    int n_launches = 0;
+    float4* accum = nullptr;
+    uchar4* rgba8 = nullptr;
+    float4 *d_nodes = nullptr, *d_tris = nullptr, *d_mats = nullptr, *d_spheres = nullptr;
+    unsigned long long* d_counters = nullptr;
+    unsigned int* d_work = nullptr;
+    int n_nodes = 0, n_spheres = 0, n_mats = 0, n_slots = 0;
+    bool scene_ok = false, cam_ok = false, counting = false;
+    float cam[12] = {0};
+    int variant = 0;
+    float last_ms = 0.0f;
+    unsigned long long last_counts[5] = {0, 0, 0, 0, 0};
+    bool count_pending = false;
+    std::string err;
+};
+
+static int fail(pt_ctx* c, int code, const std::string& msg) {
+    if (c) c->err = msg;
+    return code;
+}
+#define HIPCHK(ctx, call)                                                                   \
+    do {                                                                                    \
+        hipError_t e_ = (call);                                                             \
+        if (e_ != hipSuccess)                                                               \
+            return fail(ctx, PT_E_HIP, std::string(#call ": ") + hipGetErrorString(e_));     \
+    } while (0)
+
+static void free_scene(pt_ctx* c) {
+    (void)hipFree(c->d_nodes); (void)hipFree(c->d_tris); (void)hipFree(c->d_mats); (void)hipFree(c->d_spheres);
+    c->d_nodes = c->d_tris = c->d_mats = c->d_spheres = nullptr;
+    c->scene_ok = false;
+}
+
+extern "C" {
+
+int pt_create(const pt_config* cfg, pt_ctx** out) {
+    if (!cfg || !out) return PT_E_ARG;
+    *out = nullptr;
+    pt_ctx* c = new pt_ctx();
+    c->cfg = *cfg;
+    if (c->cfg.rays_per_pixel <= 0) c->cfg.rays_per_pixel = 1;
+    if (c->cfg.world <= 0) c->cfg.world = 1;
+    *out = c;
+    if (cfg->width <= 0 || cfg->height <= 0 || cfg->width > 65536 || cfg->height > 65536)
+        return fail(c, PT_E_ARG, "width/height out of range");
+    if (cfg->display_mode < 1 || cfg->display_mode > 4) return fail(c, PT_E_ARG, "display_mode must be 1..4");
+    if (cfg->max_bounce < 0) return fail(c, PT_E_ARG, "max_bounce must be >= 0");
+    if (c->cfg.rank < 0 || c->cfg.rank >= c->cfg.world) return fail(c, PT_E_ARG, "rank out of range");
+    int ndev = 0;
+    HIPCHK(c, hipGetDeviceCount(&ndev));
+    if (cfg->device < 0 || cfg->device >= ndev) return fail(c, PT_E_HIP, "no such HIP device");
+    HIPCHK(c, hipSetDevice(cfg->device));
+    int rank = c->cfg.rank, world = c->cfg.world;
+    c->rows_local = cfg->height > rank ? (cfg->height - rank + world - 1) / world : 0;
+    size_t px = (size_t)c->rows_local * cfg->width;
+    HIPCHK(c, hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+    HIPCHK(c, hipMalloc(&c->accum, std::max<size_t>(px, 1) * sizeof(float4)));
+    HIPCHK(c, hipMemset(c->accum, 0, std::max<size_t>(px, 1) * sizeof(float4)));
+    HIPCHK(c, hipMalloc(&c->rgba8, std::max<size_t>(px, 1) * sizeof(uchar4)));
+    HIPCHK(c, hipMalloc(&c->d_counters, 8 * sizeof(unsigned long long)));
+    HIPCHK(c, hipMalloc(&c->d_work, 64));
+    // default camera (ogl_path_trace.h:53-54)
+    const float defcam[12] = {0, -6, 1, 0, 0, 1, 0, 0, 0, 0, 0, 0};
+    pt_set_camera(c, defcam);
+    return PT_OK;
+}
+
+void pt_destroy(pt_ctx* c) {
+    if (!c) return;
+    if (c->stream) (void)hipStreamSynchronize(c->stream);
+    free_scene(c);
+    (void)hipFree(c->accum); (void)hipFree(c->rgba8); (void)hipFree(c->d_counters); (void)hipFree(c->d_work);
+    for (auto& pr : c->ev_pending) { c->ev_free.push_back(pr.first); c->ev_free.push_back(pr.second); }
+    for (hipEvent_t e : c->ev_free) (void)hipEventDestroy(e);
+    if (c->stream) (void)hipStreamDestroy(c->stream);
+    delete c;
+}
+
+const char* pt_last_error(const pt_ctx* c) { return c ? c->err.c_str() : "null context"; }
+
+int pt_upload_scene(pt_ctx* c, const float* tris, int n_tris, const float* bvh, int n_nodes,
+                    const float* mats, int n_mats, const float* spheres, int n_spheres) {
+    if (!c) return PT_E_ARG;
+    if (n_tris < 0 || n_nodes < 0 || n_mats < 0 || n_spheres < 0) return fail(c, PT_E_ARG, "negative count");
+    if ((n_tris && !tris) || (n_nodes && !bvh) || (n_mats && !mats) || (n_spheres && !spheres))
+        return fail(c, PT_E_ARG, "null array with nonzero count");
+    if (n_nodes > (1 << 24) || n_tris > (1 << 24)) return fail(c, PT_E_SCENE, "scene exceeds 2^24 records");
+    if (n_mats == 0 && (n_nodes > 0 || n_spheres > 0)) return fail(c, PT_E_SCENE, "no materials");
+    HIPCHK(c, hipSetDevice(c->cfg.device));
+    // --- validate the threaded BVH (every walk must terminate; leaves hit == miss)
+    std::vector<float4> dn(2 * (size_t)std::max(n_nodes, 1));
+    std::vector<int> leaf_slot(n_nodes, -1);
+    int n_leaves = 0;
+    for (int i = 0; i < n_nodes; i++) {
+        const float* nd = bvh + 12 * (size_t)i;
+        bool leaf = nd[8] > -1.0f;
+        int hl = (int)nd[10], ml = (int)nd[11];
+        if (hl < -1 || hl >= n_nodes || ml < -1 || ml >= n_nodes)
+            return fail(c, PT_E_SCENE, "BVH link out of range at node " + std::to_string(i));
+        if (leaf) {
+            int t0 = (int)nd[8], t1 = (int)nd[9];
+            if (t0 < 0 || t0 >= n_tris || t1 < 0 || t1 >= n_tris)
+                return fail(c, PT_E_SCENE, "leaf triangle index out of range at node " + std::to_string(i));
+            if (hl != ml) return fail(c, PT_E_SCENE, "leaf with hit link != miss link is unsupported");
+            leaf_slot[i] = n_leaves++;
+        } else if (hl < 0) {
+            return fail(c, PT_E_SCENE, "internal node without a hit link at node " + std::to_string(i));
+        }
+    }
+    // acyclicity of the (hit, miss) link graph reachable from node 0
+    if (n_nodes > 0) {
+        std::vector<unsigned char> color(n_nodes, 0);
+        std::vector<std::pair<int, int>> st;
+        st.emplace_back(0, 0);
+        color[0] = 1;
+        while (!st.empty()) {
+            auto& top = st.back();
+            const float* nd = bvh + 12 * (size_t)top.first;
+            if (top.second >= 2) { color[top.first] = 2; st.pop_back(); continue; }
+            int nx = (int)nd[10 + top.second];
+            top.second++;
+            if (nx < 0) continue;
+            if (color[nx] == 1) return fail(c, PT_E_SCENE, "BVH links form a cycle");
+            if (color[nx] == 0) { color[nx] = 1; st.emplace_back(nx, 0); }
+        }
+    }
+    for (int i = 0; i < n_tris; i++) {
+        int m = (int)tris[16 * (size_t)i + 12];
+        if (m < 0 || m >= n_mats) return fail(c, PT_E_SCENE, "triangle material index out of range");
+    }
+    for (int i = 0; i < n_spheres; i++) {
+        int m = (int)spheres[8 * (size_t)i + 4];
+        if (m < 0 || m >= n_mats) return fail(c, PT_E_SCENE, "sphere material index out of range");
+    }
+    // --- transpose to device layouts
+    std::vector<float4> dt(8 * (size_t)std::max(n_leaves, 1));
+    auto put_tri = [&](float4* q, int ti) {
+        const float* t = tris + 16 * (size_t)ti;
+        f3 v0 = mk(t[0], t[1], t[2]), v1 = mk(t[4], t[5], t[6]), v2 = mk(t[8], t[9], t[10]);
+        f3 n = pt::normalize(pt::cross(v1 - v0, v2 - v0));
+        float d0 = -pt::dot(n, v0);
+        int m = (int)t[12];
+        q[0] = make_float4(v0.x, v0.y, v0.z, n.x);
+        q[1] = make_float4(v1.x, v1.y, v1.z, n.y);
+        q[2] = make_float4(v2.x, v2.y, v2.z, n.z);
+        float mb;
+        std::memcpy(&mb, &m, 4);
+        q[3] = make_float4(d0, mb, 0.0f, 0.0f);
+    };
+    for (int i = 0; i < n_nodes; i++) {
+        const float* nd = bvh + 12 * (size_t)i;
+        int a, b;
+        if (leaf_slot[i] >= 0) {
+            int s = leaf_slot[i];
+            int t0 = (int)nd[8], t1 = (int)nd[9];
+            put_tri(&dt[8 * (size_t)s], t0);
+            put_tri(&dt[8 * (size_t)s + 4], t1);
+            a = ~((s << 1) | (t0 == t1 ? 1 : 0));
+            b = (int)nd[11];
+        } else {
+            a = (int)nd[10];
+            b = (int)nd[11];
+        }
+        float fa, fb;
+        std::memcpy(&fa, &a, 4);
+        std::memcpy(&fb, &b, 4);
+        dn[2 * (size_t)i] = make_float4(nd[0], nd[1], nd[2], fa);
+        dn[2 * (size_t)i + 1] = make_float4(nd[4], nd[5], nd[6], fb);
+    }
+    std::vector<float4> dm(3 * (size_t)std::max(n_mats, 1));
+    for (int i = 0; i < n_mats; i++) {
+        const float* m = mats + 16 * (size_t)i;
+        float s = m[12];
+        dm[3 * (size_t)i] = make_float4(m[0], m[1], m[2], m[13]);
+        dm[3 * (size_t)i + 1] = make_float4(m[4] * s, m[5] * s, m[6] * s, m[14]);
+        dm[3 * (size_t)i + 2] = make_float4(m[8], m[9], m[10], 0.0f);
+    }
+    std::vector<float4> ds(2 * (size_t)std::max(n_spheres, 1));
+    for (int i = 0; i < n_spheres; i++) {
+        const float* s = spheres + 8 * (size_t)i;
+        int m = (int)s[4];
+        float mb;
+        std::memcpy(&mb, &m, 4);
+        ds[2 * (size_t)i] = make_float4(s[0], s[1], s[2], s[3] * s[3]);
+        ds[2 * (size_t)i + 1] = make_float4(mb, 0, 0, 0);
+    }
+    free_scene(c);
+    HIPCHK(c, hipMalloc(&c->d_nodes, dn.size() * sizeof(float4)));
+    HIPCHK(c, hipMalloc(&c->d_tris, dt.size() * sizeof(float4)));
+    HIPCHK(c, hipMalloc(&c->d_mats, dm.size() * sizeof(float4)));
+    HIPCHK(c, hipMalloc(&c->d_spheres, ds.size() * sizeof(float4)));
+    HIPCHK(c, hipMemcpy(c->d_nodes, dn.data(), dn.size() * sizeof(float4), hipMemcpyHostToDevice));
+    HIPCHK(c, hipMemcpy(c->d_tris, dt.data(), dt.size() * sizeof(float4), hipMemcpyHostToDevice));
+    HIPCHK(c, hipMemcpy(c->d_mats, dm.data(), dm.size() * sizeof(float4), hipMemcpyHostToDevice));
+    HIPCHK(c, hipMemcpy(c->d_spheres, ds.data(), ds.size() * sizeof(float4), hipMemcpyHostToDevice));
+    c->n_nodes = n_nodes;
+    c->n_spheres = n_spheres;
+    c->n_mats = n_mats;
+    c->n_slots = 2 * n_leaves;
+    c->scene_ok = true;
+    return PT_OK;
+}
+
+int pt_set_camera(pt_ctx* c, const float cam[12]) {
+    if (!c || !cam) return PT_E_ARG;
+    // camera basis (computeShader.c:519-522), evaluated once per dispatch on the host with
+    // the same pinned binary32 ops the shader performs per invocation.
+    f3 pos = mk(cam[0], cam[1], cam[2]);
+    f3 fwd = pt::normalize(mk(cam[4], cam[5], cam[6]));
+    f3 right = pt::normalize(pt::cross(fwd, mk(0, 0, 1)));
+    f3 up = (pt::normalize(pt::cross(right, fwd)) * (float)c->cfg.height) / (float)c->cfg.width;
+    float v[12] = {pos.x, pos.y, pos.z, fwd.x, fwd.y, fwd.z, right.x, right.y, right.z, up.x, up.y, up.z};
+    std::memcpy(c->cam, v, sizeof(v));
+    c->cam_ok = true;
+    return PT_OK;
+}
+
+int pt_set_counting(pt_ctx* c, int enable) {
+    if (!c) return PT_E_ARG;
+    c->counting = enable != 0;
+    return PT_OK;
+}
+
+int pt_set_kernel(pt_ctx* c, int variant) {
+    if (!c) return PT_E_ARG;
+    if (variant < 0 || variant > 0) return fail(c, PT_E_ARG, "unknown kernel variant");
+    c->variant = variant;
+    return PT_OK;
+}
+
+int pt_render_async(pt_ctx* c, int frame_first, int n_frames, int acc_first) {
+    if (!c) return PT_E_ARG;
+    if (!c->scene_ok) return fail(c, PT_E_STATE, "pt_render before pt_upload_scene");
+    if (n_frames <= 0) return fail(c, PT_E_ARG, "n_frames must be > 0");
+    HIPCHK(c, hipSetDevice(c->cfg.device));
+    KParams p;
+    std::memset(&p, 0, sizeof(p));
+    p.sc.nodes = c->d_nodes;
+    p.sc.tris = c->d_tris;
+    p.sc.mats = c->d_mats;
+    p.sc.spheres = c->d_spheres;
+    p.sc.n_nodes = c->n_nodes;
+    p.sc.n_spheres = c->n_spheres;
+    p.accum = c->accum;
+    std::memcpy(p.cam, c->cam, sizeof(p.cam));
+    p.W = c->cfg.width;
+    p.H = c->cfg.height;
+    p.row0 = c->cfg.rank;
+    p.row_stride = c->cfg.world;
+    p.rows_local = c->rows_local;
+    p.x_limit = (c->cfg.flags & PT_FLAG_REF_DISPATCH) ? (p.W / 10) * 10 : p.W;
+    p.y_limit = (c->cfg.flags & PT_FLAG_REF_DISPATCH) ? (p.H / 10) * 10 : p.H;
+    p.frame_first = frame_first;
+    p.n_frames = n_frames;
+    p.acc_first = acc_first;
+    p.max_bounce = c->cfg.max_bounce;
+    p.mode = c->cfg.display_mode;
+    p.flags = c->cfg.flags;
+    p.rpp = c->cfg.rays_per_pixel;
+    p.counters = c->d_counters;
+    p.work_counter = c->d_work;
+    if (c->counting) HIPCHK(c, hipMemsetAsync(c->d_counters, 0, 8 * sizeof(unsigned long long), c->stream));
+    if (c->rows_local == 0) return PT_OK;
+    dim3 grid((p.W + 15) / 16, (c->rows_local + 15) / 16);
+    hipEvent_t ev[2];
+    for (int i = 0; i < 2; i++) {
+        if (c->ev_free.empty()) {
+            HIPCHK(c, hipEventCreate(&ev[i]));
+        } else {
+            ev[i] = c->ev_free.back();
+            c->ev_free.pop_back();
+        }
+    }
+    c->ev_pending.emplace_back(ev[0], ev[1]);
+    HIPCHK(c, hipEventRecord(ev[0], c->stream));
+    if (c->counting)
+        hipLaunchKernelGGL(k_render_tiled<true>, grid, dim3(256), 0, c->stream, p);
+    else
+        hipLaunchKernelGGL(k_render_tiled<false>, grid, dim3(256), 0, c->stream, p);
+    HIPCHK(c, hipGetLastError());
+    HIPCHK(c, hipEventRecord(ev[1], c->stream));
+    c->count_pending = c->counting;
+    return PT_OK;
+}
+
+int pt_sync(pt_ctx* c) {
+    if (!c) return PT_E_ARG;
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    for (auto& pr : c->ev_pending) {
+        float ms = 0;
+        HIPCHK(c, hipEventElapsedTime(&ms, pr.first, pr.second));
+        c->last_ms = ms;
+        c->total_ms += ms;
+        c->n_launches++;
+        c->ev_free.push_back(pr.first);
+        c->ev_free.push_back(pr.second);
+    }
+    c->ev_pending.clear();
+    if (c->count_pending) {
+        HIPCHK(c, hipMemcpy(c->last_counts, c->d_counters, 5 * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+        c->count_pending = false;
+    }
+    return PT_OK;
+}
+
+int pt_render(pt_ctx* c, int frame_first, int n_frames, int acc_first) {
+    int rc = pt_render_async(c, frame_first, n_frames, acc_first);
+    if (rc) return rc;
+    return pt_sync(c);
+}
+
+int pt_rows(const pt_ctx* c, int* rows_local, int* row0, int* row_stride) {
+    if (!c) return PT_E_ARG;
+    if (rows_local) *rows_local = c->rows_local;
+    if (row0) *row0 = c->cfg.rank;
+    if (row_stride) *row_stride = c->cfg.world;
+    return PT_OK;
+}
+
+int pt_read_rgba32f(pt_ctx* c, float* dst, size_t bytes) {
+    if (!c || !dst) return PT_E_ARG;
+    size_t need = (size_t)c->rows_local * c->cfg.width * sizeof(float4);
+    if (bytes < need) return fail(c, PT_E_ARG, "destination too small");
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    HIPCHK(c, hipMemcpy(dst, c->accum, need, hipMemcpyDeviceToHost));
+    return PT_OK;
+}
+
+int pt_write_rgba32f(pt_ctx* c, const float* src, size_t bytes) {
+    if (!c || !src) return PT_E_ARG;
+    size_t need = (size_t)c->rows_local * c->cfg.width * sizeof(float4);
+    if (bytes < need) return fail(c, PT_E_ARG, "source too small");
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    HIPCHK(c, hipMemcpy(c->accum, src, need, hipMemcpyHostToDevice));
+    return PT_OK;
+}
+
+int pt_read_rgba8_aces(pt_ctx* c, unsigned char* dst, size_t bytes) {
+    if (!c || !dst) return PT_E_ARG;
+    long long n = (long long)c->rows_local * c->cfg.width;
+    if (bytes < (size_t)n * 4) return fail(c, PT_E_ARG, "destination too small");
+    if (n == 0) return PT_OK;
+    hipLaunchKernelGGL(k_aces, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, c->stream, c->accum, c->rgba8, n);
+    HIPCHK(c, hipGetLastError());
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    HIPCHK(c, hipMemcpy(dst, c->rgba8, (size_t)n * 4, hipMemcpyDeviceToHost));
+    return PT_OK;
+}
+
+int pt_accum_device(pt_ctx* c, void** ptr, size_t* bytes) {
+    if (!c) return PT_E_ARG;
+    if (ptr) *ptr = c->accum;
+    if (bytes) *bytes = (size_t)c->rows_local * c->cfg.width * sizeof(float4);
+    return PT_OK;
+}
+
+int pt_copy_rows_device(pt_ctx* c, void* dst, size_t bytes) {
+    if (!c || !dst) return PT_E_ARG;
+    size_t need = (size_t)c->rows_local * c->cfg.width * sizeof(float4);
+    if (bytes < need) return fail(c, PT_E_ARG, "destination too small");
+    HIPCHK(c, hipMemcpyAsync(dst, c->accum, need, hipMemcpyDeviceToDevice, c->stream));
+    return pt_sync(c);
+}
+
+int pt_timing(pt_ctx* c, double* total_ms, int* n, int reset) {
+    if (!c) return PT_E_ARG;
+    if (total_ms) *total_ms = c->total_ms;
+    if (n) *n = c->n_launches;
+    if (reset) { c->total_ms = 0.0; c->n_launches = 0; }
+    return PT_OK;
+}
+
+int pt_stream(pt_ctx* c, void** s) {
+    if (!c || !s) return PT_E_ARG;
+    *s = (void*)c->stream;
+    return PT_OK;
+}
+
+int pt_stats(pt_ctx* c, double* ms, unsigned long long out[5]) {
+    if (!c) return PT_E_ARG;
+    if (ms) *ms = c->last_ms;
+    if (out) std::memcpy(out, c->last_counts, sizeof(c->last_counts));
+    return PT_OK;
+}
+
+}  // extern "C"

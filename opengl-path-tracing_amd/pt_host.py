@@ -1,0 +1,320 @@
+"""Python mirror of the reference's host interface for the hot path, over the pt_api.h /
+pt_scene.h C ABI (ctypes; build/libptrace.so).
+
+Names follow the reference so that its call sequence reads the same:
+  load_vertex_data(obj, mtl)  geometry_loader.h:15-142   -> (tris[N,16], mats[M,16])
+  buildSAHTree(tris)          bvh.h:255-268              -> nodes[K,12]
+  setupBuffers(obj, mtl)      ogl_path_trace.h:367-530   -> SceneBuffers (5 std140 buffers)
+  ComputeShader / PathTracer  shader_c.h + glDispatchCompute(ogl_path_trace.h:174-186)
+    .dispatch(frame, accumulate)        one reference dispatch (uniforms frame/accumulate)
+    .render(frame_first, n, acc_first)  n dispatches fused in one launch (bit-identical)
+Errors raise PTError carrying the library's code and message (the reference prints and
+continues; the drop-in fails loudly instead -- DESIGN.md §2.4).
+
+There is no CPU fallback: if the HIP library is missing or no device is present, the
+calls raise.  The CPU oracle lives in oracle/ and is only used by tests and the bench's
+cpu_baseline leg.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+
+PKG_DIR = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(PKG_DIR, "build", "libptrace.so")
+INCLUDE_DIR = os.path.join(os.path.dirname(PKG_DIR), "include")
+
+PT_FLAG_NO_AA, PT_FLAG_NO_SKY, PT_FLAG_NO_SPHERES, PT_FLAG_NO_TRIANGLES, PT_FLAG_REF_DISPATCH = 1, 2, 4, 8, 16
+DEFAULT_CAMERA = np.array([0, -6, 1, 0, 0, 1, 0, 0, 0, 0, 0, 0], np.float32)  # ogl_path_trace.h:53-54
+
+_ERR = {-1: "PT_E_ARG", -2: "PT_E_IO", -3: "PT_E_PARSE", -4: "PT_E_SCENE", -5: "PT_E_HIP", -6: "PT_E_STATE"}
+
+
+class PTError(RuntimeError):
+    def __init__(self, code, msg):
+        super().__init__("%s (%d): %s" % (_ERR.get(code, "PT_E?"), code, msg))
+        self.code = code
+
+
+class _Config(C.Structure):
+    _fields_ = [(n, C.c_int) for n in ("width", "height", "max_bounce", "display_mode", "flags",
+                                       "rays_per_pixel", "device", "rank", "world")]
+
+
+_lib = None
+_F = np.ctypeslib.ndpointer(np.float32, flags="C_CONTIGUOUS")
+
+
+def build(force=False):
+    """Compile build/libptrace.so (hipcc, gfx950) in-tree."""
+    if force or not os.path.exists(LIB_PATH):
+        subprocess.check_call(["make", "-s", "-C", PKG_DIR, "all"])
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise PTError(-5, "native library %s is missing; run `make -C %s`" % (LIB_PATH, PKG_DIR))
+        L = C.CDLL(LIB_PATH)
+        vp, ip, fp = C.c_void_p, C.c_int, C.c_float
+        sig = {
+            "pt_scene_load_obj": (ip, [C.c_char_p, C.c_char_p, C.POINTER(vp)]),
+            "pt_scene_from_arrays": (ip, [_F, ip, _F, ip, C.POINTER(vp)]),
+            "pt_scene_add_builtins": (ip, [vp]),
+            "pt_scene_build_bvh": (ip, [vp]),
+            "pt_scene_counts": (ip, [vp, np.ctypeslib.ndpointer(np.int32)]),
+            "pt_scene_get_tris": (ip, [vp, _F, ip]),
+            "pt_scene_get_mats": (ip, [vp, _F, ip]),
+            "pt_scene_get_spheres": (ip, [vp, _F, ip]),
+            "pt_scene_get_nodes": (ip, [vp, _F, ip]),
+            "pt_scene_last_error": (C.c_char_p, [vp]),
+            "pt_scene_free": (None, [vp]),
+            "pt_bvh_build": (ip, [_F, ip, _F, ip, C.POINTER(ip)]),
+            "pt_aces_rgba8_host": (None, [_F, C.c_longlong, np.ctypeslib.ndpointer(np.uint8)]),
+            "pt_create": (ip, [C.POINTER(_Config), C.POINTER(vp)]),
+            "pt_destroy": (None, [vp]),
+            "pt_last_error": (C.c_char_p, [vp]),
+            "pt_upload_scene": (ip, [vp, _F, ip, _F, ip, _F, ip, _F, ip]),
+            "pt_set_camera": (ip, [vp, _F]),
+            "pt_render": (ip, [vp, ip, ip, ip]),
+            "pt_render_async": (ip, [vp, ip, ip, ip]),
+            "pt_sync": (ip, [vp]),
+            "pt_rows": (ip, [vp, C.POINTER(ip), C.POINTER(ip), C.POINTER(ip)]),
+            "pt_read_rgba32f": (ip, [vp, vp, C.c_size_t]),
+            "pt_read_rgba8_aces": (ip, [vp, vp, C.c_size_t]),
+            "pt_write_rgba32f": (ip, [vp, vp, C.c_size_t]),
+            "pt_accum_device": (ip, [vp, C.POINTER(vp), C.POINTER(C.c_size_t)]),
+            "pt_stream": (ip, [vp, C.POINTER(vp)]),
+            "pt_set_counting": (ip, [vp, ip]),
+            "pt_stats": (ip, [vp, C.POINTER(C.c_double), np.ctypeslib.ndpointer(np.uint64)]),
+            "pt_set_kernel": (ip, [vp, ip]),
+            "pt_copy_rows_device": (ip, [vp, vp, C.c_size_t]),
+            "pt_timing": (ip, [vp, C.POINTER(C.c_double), C.POINTER(ip), ip]),
+        }
+        for name, (res, args) in sig.items():
+            fn = getattr(L, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = L
+    return _lib
+
+
+def header_symbols():
+    """Function names declared in include/*.h (for the ABI export test)."""
+    import re
+    names = []
+    for h in ("pt_api.h", "pt_scene.h"):
+        txt = open(os.path.join(INCLUDE_DIR, h)).read()
+        txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
+        names += re.findall(r"\b(pt_[a-z0-9_]+)\s*\(", txt)
+    return sorted(set(names))
+
+
+# ----------------------------------------------------------------------------- scene ingest
+def _f32(a, cols):
+    a = np.ascontiguousarray(a, np.float32)
+    return a.reshape(-1, cols) if a.size else np.zeros((0, cols), np.float32)
+
+
+class _Scene:
+    def __init__(self, handle):
+        self.h = handle
+
+    def __del__(self):
+        if getattr(self, "h", None):
+            lib().pt_scene_free(self.h)
+            self.h = None
+
+    def check(self, rc):
+        if rc:
+            raise PTError(rc, lib().pt_scene_last_error(self.h).decode())
+
+    def counts(self):
+        c = np.zeros(5, np.int32)
+        self.check(lib().pt_scene_counts(self.h, c))
+        return dict(n_tris=int(c[0]), n_mats=int(c[1]), n_spheres=int(c[2]), n_nodes=int(c[3]), n_loaded_mats=int(c[4]))
+
+    def arrays(self):
+        c = self.counts()
+        out = {}
+        for key, n, cols, fn in (("tris", c["n_tris"], 16, lib().pt_scene_get_tris),
+                                 ("mats", c["n_mats"], 16, lib().pt_scene_get_mats),
+                                 ("spheres", c["n_spheres"], 8, lib().pt_scene_get_spheres),
+                                 ("nodes", c["n_nodes"], 12, lib().pt_scene_get_nodes)):
+            a = np.zeros((max(n, 1), cols), np.float32)
+            self.check(fn(self.h, a, max(n, 1)))
+            out[key] = a[:n].copy()
+        out["n_loaded_mats"] = c["n_loaded_mats"]
+        return out
+
+
+def load_vertex_data(obj_path, mtl_path):
+    """geometry_loader.h:15 -> (tris[N,16], mats[M,16]) float32 std140 records."""
+    h = C.c_void_p()
+    rc = lib().pt_scene_load_obj(str(obj_path).encode(), str(mtl_path).encode(), C.byref(h))
+    s = _Scene(h)
+    s.check(rc)
+    a = s.arrays()
+    return a["tris"], a["mats"]
+
+
+def buildSAHTree(tris):
+    """bvh.h:255 -> nodes[K,12] {min, max, {tri0, tri1, hit, miss}} (preorder-pair layout)."""
+    tris = _f32(tris, 16)
+    n = len(tris)
+    out = np.zeros((max(2 * n, 1), 12), np.float32)
+    nn = C.c_int()
+    rc = lib().pt_bvh_build(tris.reshape(-1) if n else np.zeros(16, np.float32), n, out.reshape(-1), len(out), C.byref(nn))
+    if rc:
+        raise PTError(rc, lib().pt_scene_last_error(None).decode())
+    return out[: nn.value].copy()
+
+
+class SceneBuffers(dict):
+    """The five SSBO contents of setupBuffers(): tris, nodes, mats, spheres, cam."""
+
+
+def setupBuffers(obj_path, mtl_path, camera=None):
+    """ogl_path_trace.h:367-530: load, build the BVH, append built-ins + metal sphere."""
+    h = C.c_void_p()
+    rc = lib().pt_scene_load_obj(str(obj_path).encode(), str(mtl_path).encode(), C.byref(h))
+    s = _Scene(h)
+    s.check(rc)
+    s.check(lib().pt_scene_add_builtins(s.h))
+    s.check(lib().pt_scene_build_bvh(s.h))
+    a = s.arrays()
+    a["cam"] = DEFAULT_CAMERA.copy() if camera is None else np.asarray(camera, np.float32).reshape(12)
+    return SceneBuffers(a)
+
+
+def scene_from_arrays(tris, mats, builtins=True, camera=None):
+    tris, mats = _f32(tris, 16), _f32(mats, 16)
+    h = C.c_void_p()
+    rc = lib().pt_scene_from_arrays(tris.reshape(-1) if len(tris) else np.zeros(16, np.float32), len(tris),
+                                    mats.reshape(-1) if len(mats) else np.zeros(16, np.float32), len(mats), C.byref(h))
+    s = _Scene(h)
+    s.check(rc)
+    if builtins:
+        s.check(lib().pt_scene_add_builtins(s.h))
+    if len(tris):
+        s.check(lib().pt_scene_build_bvh(s.h))
+    a = s.arrays()
+    a["cam"] = DEFAULT_CAMERA.copy() if camera is None else np.asarray(camera, np.float32).reshape(12)
+    return SceneBuffers(a)
+
+
+def aces_rgba8_host(img):
+    img = np.ascontiguousarray(img, np.float32)
+    out = np.zeros(img.shape[:-1] + (4,), np.uint8)
+    lib().pt_aces_rgba8_host(img.reshape(-1), img.size // 4, out.reshape(-1))
+    return out
+
+
+# ----------------------------------------------------------------------------- renderer
+class PathTracer:
+    """The compute program + its image: pt_create / pt_upload_scene / pt_render."""
+
+    def __init__(self, width, height, max_bounce=5, display_mode=1, flags=0, rays_per_pixel=1,
+                 device=0, rank=0, world=1):
+        cfg = _Config(width, height, max_bounce, display_mode, flags, rays_per_pixel, device, rank, world)
+        h = C.c_void_p()
+        rc = lib().pt_create(C.byref(cfg), C.byref(h))
+        self.h = h
+        self.width, self.height = width, height
+        self._check(rc)
+        rl, r0, rs = C.c_int(), C.c_int(), C.c_int()
+        self._check(lib().pt_rows(self.h, C.byref(rl), C.byref(r0), C.byref(rs)))
+        self.rows_local, self.row0, self.row_stride = rl.value, r0.value, rs.value
+
+    def _check(self, rc):
+        if rc:
+            raise PTError(rc, lib().pt_last_error(self.h).decode())
+
+    def close(self):
+        if getattr(self, "h", None):
+            lib().pt_destroy(self.h)
+            self.h = None
+
+    __del__ = close
+
+    def upload(self, sb):
+        t, n, m, s = _f32(sb["tris"], 16), _f32(sb["nodes"], 12), _f32(sb["mats"], 16), _f32(sb["spheres"], 8)
+        z = lambda a, c: a.reshape(-1) if a.size else np.zeros(c, np.float32)
+        self._check(lib().pt_upload_scene(self.h, z(t, 16), len(t), z(n, 12), len(n), z(m, 16), len(m), z(s, 8), len(s)))
+        if "cam" in sb:
+            self.set_camera(sb["cam"])
+
+    def set_camera(self, cam):
+        self._check(lib().pt_set_camera(self.h, np.ascontiguousarray(cam, np.float32).reshape(12)))
+
+    def set_counting(self, on=True):
+        self._check(lib().pt_set_counting(self.h, int(bool(on))))
+
+    def set_kernel(self, variant):
+        self._check(lib().pt_set_kernel(self.h, int(variant)))
+
+    def dispatch(self, frame, accumulate):
+        """One glDispatchCompute with uniforms frame/accumulate (ogl_path_trace.h:176-183)."""
+        self._check(lib().pt_render(self.h, frame, 1, accumulate))
+
+    def render(self, frame_first, n_frames, accumulate_first):
+        self._check(lib().pt_render(self.h, frame_first, n_frames, accumulate_first))
+
+    def render_async(self, frame_first, n_frames, accumulate_first):
+        self._check(lib().pt_render_async(self.h, frame_first, n_frames, accumulate_first))
+
+    def sync(self):
+        self._check(lib().pt_sync(self.h))
+
+    def read_rgba32f(self):
+        out = np.zeros((self.rows_local, self.width, 4), np.float32)
+        self._check(lib().pt_read_rgba32f(self.h, out.ctypes.data, out.nbytes))
+        return out
+
+    def write_rgba32f(self, img):
+        img = np.ascontiguousarray(img, np.float32)
+        self._check(lib().pt_write_rgba32f(self.h, img.ctypes.data, img.nbytes))
+
+    def read_rgba8(self):
+        out = np.zeros((self.rows_local, self.width, 4), np.uint8)
+        self._check(lib().pt_read_rgba8_aces(self.h, out.ctypes.data, out.nbytes))
+        return out
+
+    def accum_device(self):
+        p, n = C.c_void_p(), C.c_size_t()
+        self._check(lib().pt_accum_device(self.h, C.byref(p), C.byref(n)))
+        return p.value, n.value
+
+    def copy_rows_device(self, dst_ptr, nbytes):
+        self._check(lib().pt_copy_rows_device(self.h, C.c_void_p(dst_ptr), nbytes))
+
+    def timing(self, reset=False):
+        ms, n = C.c_double(), C.c_int()
+        self._check(lib().pt_timing(self.h, C.byref(ms), C.byref(n), int(bool(reset))))
+        return ms.value, n.value
+
+    def stream(self):
+        s = C.c_void_p()
+        self._check(lib().pt_stream(self.h, C.byref(s)))
+        return s.value
+
+    def stats(self):
+        ms = C.c_double()
+        cnt = np.zeros(5, np.uint64)
+        self._check(lib().pt_stats(self.h, C.byref(ms), cnt))
+        return ms.value, dict(segments=int(cnt[0]), node_visits=int(cnt[1]), tri_tests=int(cnt[2]),
+                              sphere_tests=int(cnt[3]), hits=int(cnt[4]))
+
+
+def assemble_rows(parts, height):
+    """Interleave per-rank local rows (rank r owns rows r, r+G, ...) into a full image."""
+    G = len(parts)
+    W = parts[0].shape[1]
+    img = np.zeros((height, W, 4), np.float32)
+    for r, p in enumerate(parts):
+        img[r::G][: len(p)] = p
+    return img

@@ -1,0 +1,133 @@
+"""HIP path vs CPU oracle: bit-exact RGBA32F parity (SURVEY.md App. B ladder, step 1).
+
+Tolerance: NONE -- every comparison is on the uint32 bit patterns (NaN payloads
+included).  The kernels and the oracle pin every binary32 operation.
+"""
+import numpy as np
+import pytest
+
+import oracle_lib as O
+import pt_host as H
+
+pytestmark = pytest.mark.gpu
+
+
+def bits(a):
+    return np.ascontiguousarray(a, np.float32).view(np.uint32)
+
+
+def assert_bitwise(got, want, label=""):
+    g, w = bits(got), bits(want)
+    bad = np.argwhere(g != w)
+    assert bad.size == 0, "%s: %d words differ; first %s got %r want %r" % (
+        label, len(bad), bad[:3].tolist(), got[tuple(bad[0])], want[tuple(bad[0])])
+
+
+def gpu_render(sc, W, H_, max_bounce=5, mode=1, frame_first=1, n_frames=1, acc_first=0,
+               flags=0, rank=0, world=1, prior=None, counting=False, variant=0):
+    pt = H.PathTracer(W, H_, max_bounce=max_bounce, display_mode=mode, flags=flags, rank=rank, world=world)
+    pt.set_kernel(variant)
+    pt.upload(sc)
+    if prior is not None:
+        pt.write_rgba32f(prior)
+    if counting:
+        pt.set_counting(True)
+    pt.render(frame_first, n_frames, acc_first)
+    img = pt.read_rgba32f()
+    st = pt.stats()
+    pt.close()
+    return (img, st) if counting else img
+
+
+@pytest.mark.parametrize("mode", [2, 3, 4])
+def test_debug_modes_bitwise(cornell_scene, mode):
+    want = O.render(cornell_scene, 64, 48, mode=mode)
+    got = gpu_render(cornell_scene, 64, 48, mode=mode)
+    assert_bitwise(got, want, "mode %d" % mode)
+
+
+@pytest.mark.parametrize("spp", [1, 4, 16])
+def test_shaded_cornell_bitwise(cornell_scene, spp):
+    want = O.render(cornell_scene, 64, 64, max_bounce=5, n_frames=spp)
+    got = gpu_render(cornell_scene, 64, 64, max_bounce=5, n_frames=spp)
+    assert_bitwise(got, want, "cornell %d spp" % spp)
+
+
+def test_shaded_ship_bitwise(ship_scene):
+    want = O.render(ship_scene, 80, 60, max_bounce=5, n_frames=4)
+    got = gpu_render(ship_scene, 80, 60, max_bounce=5, n_frames=4)
+    assert_bitwise(got, want, "ship")
+
+
+def test_eight_bounces_and_frame_offset(cornell_scene):
+    # frames 3000..3002 exercise the signed-overflow seed term (frame*719393 > 2^31)
+    prior = np.random.default_rng(1).random((36, 64, 4), dtype=np.float32)
+    want = O.render(cornell_scene, 64, 36, max_bounce=8, frame_first=3000, n_frames=3, acc_first=1,
+                    accum=prior.copy())
+    got = gpu_render(cornell_scene, 64, 36, max_bounce=8, frame_first=3000, n_frames=3, acc_first=1,
+                     prior=prior)
+    assert_bitwise(got, want, "8 bounces")
+
+
+def test_fused_equals_separate_dispatches(cornell_scene):
+    pt = H.PathTracer(48, 32, max_bounce=8)
+    pt.upload(cornell_scene)
+    for f in range(1, 6):
+        pt.dispatch(f, 0 if f == 1 else 1)
+    sep = pt.read_rgba32f()
+    pt.render(1, 5, 0)
+    fused = pt.read_rgba32f()
+    pt.close()
+    assert_bitwise(fused, sep, "fused vs separate")
+
+
+@pytest.mark.parametrize("flags", [H.PT_FLAG_NO_AA, H.PT_FLAG_NO_SKY, H.PT_FLAG_NO_SPHERES,
+                                   H.PT_FLAG_NO_TRIANGLES])
+def test_toggles_bitwise(cornell_scene, flags):
+    want = O.render(cornell_scene, 40, 30, n_frames=2, flags=flags)
+    got = gpu_render(cornell_scene, 40, 30, n_frames=2, flags=flags)
+    assert_bitwise(got, want, "flags %d" % flags)
+
+
+def test_ref_dispatch_footprint(cornell_scene):
+    # glDispatchCompute(W/10, H/10) with 10x10 groups writes only the 250x250 block at 256^2
+    got = gpu_render(cornell_scene, 256, 256, mode=2, flags=H.PT_FLAG_REF_DISPATCH)
+    assert np.all(got[250:] == 0) and np.all(got[:, 250:] == 0)
+    want = O.render(cornell_scene, 256, 256, mode=2)
+    assert_bitwise(got[:250, :250], want[:250, :250], "footprint")
+
+
+def test_partition_invariance(cornell_scene):
+    full = gpu_render(cornell_scene, 64, 50, max_bounce=8, n_frames=3)
+    parts = [gpu_render(cornell_scene, 64, 50, max_bounce=8, n_frames=3, rank=r, world=3) for r in range(3)]
+    assert_bitwise(H.assemble_rows(parts, 50), full, "3-way row split")
+
+
+def test_counters_match_oracle(cornell_scene):
+    want_img, want_cnt = O.render(cornell_scene, 48, 48, max_bounce=8, n_frames=4, counters=True)
+    got_img, (ms, cnt) = gpu_render(cornell_scene, 48, 48, max_bounce=8, n_frames=4, counting=True)
+    assert_bitwise(got_img, want_img, "counting build")
+    assert [cnt["segments"], cnt["node_visits"], cnt["tri_tests"], cnt["sphere_tests"], cnt["hits"]] == \
+        [int(x) for x in want_cnt]
+
+
+def test_full_hd_sampled_pixels(cornell_scene):
+    """1920x1080, 8 bounces, 2 spp: the full-size GPU frame checked bit-exactly at 4000
+    oracle-rendered pixels (plus every pixel of the first and last rows)."""
+    W, Hh = 1920, 1080
+    got = gpu_render(cornell_scene, W, Hh, max_bounce=8, n_frames=2)
+    rng = np.random.default_rng(7)
+    xs = np.concatenate([rng.integers(0, W, 4000), np.arange(W), np.arange(W)])
+    ys = np.concatenate([rng.integers(0, Hh, 4000), np.zeros(W, int), np.full(W, Hh - 1)])
+    want = O.render_pixels(cornell_scene, W, Hh, xs, ys, max_bounce=8, n_frames=2)
+    assert_bitwise(got[ys, xs], want, "1080p samples")
+
+
+def test_aces_epilogue(cornell_scene):
+    pt = H.PathTracer(64, 64, max_bounce=5)
+    pt.upload(cornell_scene)
+    pt.render(1, 8, 0)
+    img = pt.read_rgba32f()
+    rgba8 = pt.read_rgba8()
+    pt.close()
+    assert np.array_equal(rgba8, O.aces_rgba8(img))
