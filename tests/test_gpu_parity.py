@@ -123,6 +123,17 @@ def test_full_hd_sampled_pixels(cornell_scene):
     assert_bitwise(got[ys, xs], want, "1080p samples")
 
 
+def test_golden_fixtures(cornell_scene, ship_scene):
+    """Committed fixtures (oracle == numpy twin, tests/golden/make_golden.py)."""
+    import os
+    z = np.load(os.path.join(os.path.dirname(__file__), "golden", "golden_images.npz"))
+    for key in z.files:
+        scene, W, Hh, mb, mode, spp = key.split("_")
+        sc = cornell_scene if scene == "cornell" else ship_scene
+        got = gpu_render(sc, int(W), int(Hh), max_bounce=int(mb), mode=int(mode), n_frames=int(spp))
+        assert_bitwise(got, z[key], key)
+
+
 def test_aces_epilogue(cornell_scene):
     pt = H.PathTracer(64, 64, max_bounce=5)
     pt.upload(cornell_scene)
