@@ -48,6 +48,8 @@ struct KParams {
     int max_bounce, mode, flags, rpp;
     unsigned long long* counters;  // [5] when counting
     unsigned int* work_counter;    // persistent kernel pixel queue
+    int n_slots, n_mats;           // triangle slots / materials (LDS staging sizes)
+    int scene_fast;                // every box coordinate inside the exact-reciprocal guard
 };
 
 struct Cnt {
@@ -268,6 +270,287 @@ __global__ __launch_bounds__(256) void k_render_tiled(KParams p) {
     flush_counters<COUNT>(p, c);
 }
 
+// =====================================================================================
+// Variant 0 (default): persistent wavefront kernel with path regeneration.
+//
+// * Work = (pixel, all n_frames of this launch); lanes pull pixels from a device queue
+//   with one wave-aggregated atomic (ballot + popcount + shfl), 8x8-pixel tiles in queue
+//   order so a wave starts on a coherent tile.
+// * Every loop iteration runs ONE segment (calculateRayCollision + shading) for every
+//   busy lane; a lane whose path ended regenerates the next frame's camera ray in the
+//   next iteration instead of idling until the wave's longest path ends.  The frames of a
+//   pixel stay in order in one lane, so the running mean is bit-identical.
+// * Slab test in exact-reciprocal form: q = RN((b-o)/d) computed as q0 = (b-o)*rd,
+//   q = fma(fma(-q0, d, b-o), rd, q0) with rd = RN(1/d) per ray (Markstein's theorem:
+//   correctly rounded when no under/overflow).  The guard that makes that hold is checked
+//   per ray (|d_i| in [2^-20, 2], origin components 0 or in [2^-40, 2^60]) and per scene
+//   (box coordinates likewise, at upload); lanes outside it use the IEEE division chain.
+//   With all quotients finite the swap/compare chain of :309-365 equals min/max form.
+// * Small scenes are staged in LDS once per workgroup (ds_read instead of vector-memory
+//   gathers on the dependent node->node chain).
+// =====================================================================================
+struct SceneView {
+    const float4* nodes;
+    const float4* tris;
+    const float4* mats;
+    const float4* spheres;
+};
+
+__device__ __forceinline__ float qdiv(float a, float b, float rb) {
+    float q = a * rb;
+    float r = __builtin_fmaf(-q, b, a);
+    return __builtin_fmaf(r, rb, q);
+}
+
+__device__ __forceinline__ bool in_guard(float v, float lo, float hi) {
+    float a = __builtin_fabsf(v);
+    return v == 0.0f || (a >= lo && a <= hi);
+}
+
+__device__ __forceinline__ bool slab_fast(float4 lo, float4 hi, f3 o, f3 d, f3 rd, float cur_t) {
+    float x0 = qdiv(lo.x - o.x, d.x, rd.x), x1 = qdiv(hi.x - o.x, d.x, rd.x);
+    float y0 = qdiv(lo.y - o.y, d.y, rd.y), y1 = qdiv(hi.y - o.y, d.y, rd.y);
+    float z0 = qdiv(lo.z - o.z, d.z, rd.z), z1 = qdiv(hi.z - o.z, d.z, rd.z);
+    float tn = fmaxf(fmaxf(fminf(x0, x1), fminf(y0, y1)), fminf(z0, z1));
+    float tf = fminf(fminf(fmaxf(x0, x1), fmaxf(y0, y1)), fmaxf(z0, z1));
+    return tn <= tf && tn <= cur_t;
+}
+
+template <bool COUNT>
+__device__ __forceinline__ bool collide_v(const SceneView& S, int n_nodes, int n_spheres, int flags,
+                                          f3 o, f3 d, bool fast, f3 rd, f3& normal, f3& hitp, int& mat,
+                                          Cnt& c) {
+    float t = __builtin_huge_valf();
+    bool hit = false;
+    if (!(flags & PT_FLAG_NO_SPHERES)) {
+        for (int si = 0; si < n_spheres; si++) {
+            float4 s0 = S.spheres[2 * si];
+            f3 cc = mk(s0.x, s0.y, s0.z);
+            f3 oc = o - cc;
+            float a = pt::dot(d, d);
+            float half_b = pt::dot(oc, d);
+            float cq = pt::dot(oc, oc) - s0.w;
+            float disc = half_b * half_b - a * cq;
+            float ht = disc < 0.0f ? -1.0f : (-half_b - pt::fsqrt(disc)) / a;
+            if (COUNT) c.sph++;
+            if (ht > 0.0001f && ht < t) {
+                f3 pn = pt::normalize((o + d * ht) - cc);
+                if (pt::dot(pn, d) > 0.0f) pn = pn * -1.0f;
+                hit = true;
+                t = ht;
+                normal = pn;
+                hitp = o + d * ht;
+                mat = __float_as_int(S.spheres[2 * si + 1].x);
+            }
+        }
+    }
+    if ((flags & PT_FLAG_NO_TRIANGLES) || n_nodes <= 0) return hit;
+    int bi = 0;
+    for (int steps = 0; bi > -1 && steps < n_nodes; steps++) {
+        float4 lo = S.nodes[2 * bi], hi = S.nodes[2 * bi + 1];
+        int a = __float_as_int(lo.w), b = __float_as_int(hi.w);
+        bool hb;
+        if (fast) hb = slab_fast(lo, hi, o, d, rd, t);
+        else hb = slab(lo, hi, o, d, t);
+        if (COUNT) c.nodes++;
+        int next = (hb && a >= 0) ? a : b;
+        if (hb && a < 0) {
+            if (COUNT) c.tri += 2;
+            int code = ~a;
+            const float4* T0 = S.tris + 8 * (code >> 1);
+            f3 n0, n1;
+            float h1 = tri_hit(T0, o, d, t, n0);
+            float h2 = h1;
+            n1 = n0;
+            if (!(code & 1)) h2 = tri_hit(T0 + 4, o, d, t, n1);
+            if (h1 > 0.0001f && h1 < t && (h1 < h2 || h2 < 0.0001f)) {
+                if (pt::dot(n0, d) > 0.0f) n0 = n0 * -1.0f;
+                hit = true;
+                t = h1;
+                normal = n0;
+                hitp = o + d * h1;
+                mat = __float_as_int(T0[3].y);
+            } else if (h2 > 0.0001f && h2 < t) {
+                if (pt::dot(n1, d) > 0.0f) n1 = n1 * -1.0f;
+                hit = true;
+                t = h2;
+                normal = n1;
+                hitp = o + d * h2;
+                mat = __float_as_int(T0[(code & 1) ? 3 : 7].y);
+            }
+        }
+        bi = next;
+    }
+    return hit;
+}
+
+template <bool COUNT, bool LDS>
+__global__ __launch_bounds__(256) void k_render_wave(KParams p) {
+    extern __shared__ float4 lds[];
+    SceneView S;
+    if (LDS) {
+        int nn = 2 * p.sc.n_nodes, nt = 4 * p.n_slots, nm = 3 * p.n_mats, ns = 2 * p.sc.n_spheres;
+        for (int i = threadIdx.x; i < nn; i += blockDim.x) lds[i] = p.sc.nodes[i];
+        for (int i = threadIdx.x; i < nt; i += blockDim.x) lds[nn + i] = p.sc.tris[i];
+        for (int i = threadIdx.x; i < nm; i += blockDim.x) lds[nn + nt + i] = p.sc.mats[i];
+        for (int i = threadIdx.x; i < ns; i += blockDim.x) lds[nn + nt + nm + i] = p.sc.spheres[i];
+        __syncthreads();
+        S.nodes = lds;
+        S.tris = lds + nn;
+        S.mats = lds + nn + nt;
+        S.spheres = lds + nn + nt + nm;
+    } else {
+        S.nodes = p.sc.nodes;
+        S.tris = p.sc.tris;
+        S.mats = p.sc.mats;
+        S.spheres = p.sc.spheres;
+    }
+    const int lane = threadIdx.x & 63;
+    const f3 cpos = mk(p.cam[0], p.cam[1], p.cam[2]), cfwd = mk(p.cam[3], p.cam[4], p.cam[5]);
+    const f3 cright = mk(p.cam[6], p.cam[7], p.cam[8]), cup = mk(p.cam[9], p.cam[10], p.cam[11]);
+    const int tiles_x = (p.W + 7) >> 3;
+    const unsigned total_ids = (unsigned)tiles_x * (unsigned)((p.rows_local + 7) >> 3) * 64u;
+    const bool origin0_ok = p.scene_fast && in_guard(cpos.x, 0x1p-40f, 0x1p60f) &&
+                            in_guard(cpos.y, 0x1p-40f, 0x1p60f) && in_guard(cpos.z, 0x1p-40f, 0x1p60f);
+
+    Cnt c = {0, 0, 0, 0, 0};
+    bool done = false, need_path = true;
+    int lx = -1, y = 0;
+    size_t aidx = 0;
+    int k = 0, r = 0, bounce = 0;
+    float4 acc = make_float4(0, 0, 0, 0);
+    f3 psum = mk(0, 0, 0), o = mk(0, 0, 0), d = mk(0, 0, 1), inc = mk(0, 0, 0), col = mk(1, 1, 1);
+    uint32_t state = 0;
+
+    for (;;) {
+        // (1) release a pixel whose frames are all done
+        if (!done && need_path && lx >= 0 && k >= p.n_frames) {
+            p.accum[aidx] = acc;
+            lx = -1;
+        }
+        // (2) wave-aggregated pull from the pixel queue
+        bool want = !done && lx < 0;
+        unsigned long long m = __ballot(want);
+        if (m) {
+            int leader = __ffsll((long long)m) - 1;
+            unsigned base = 0;
+            if (lane == leader) base = atomicAdd(p.work_counter, (unsigned)__popcll(m));
+            base = __shfl(base, leader, 64);
+            if (want) {
+                unsigned id = base + (unsigned)__popcll(m & ((1ull << lane) - 1ull));
+                if (id >= total_ids) {
+                    done = true;
+                } else {
+                    unsigned tile = id >> 6, w = id & 63u;
+                    int cx = (int)(tile % (unsigned)tiles_x) * 8 + (int)(w & 7u);
+                    int crow = (int)(tile / (unsigned)tiles_x) * 8 + (int)(w >> 3);
+                    int cy = p.row0 + crow * p.row_stride;
+                    if (cx < p.W && crow < p.rows_local && cx < p.x_limit && cy < p.y_limit) {
+                        lx = cx;
+                        y = cy;
+                        aidx = (size_t)crow * p.W + cx;
+                        k = 0;
+                        r = 0;
+                        psum = mk(0, 0, 0);
+                        acc = p.acc_first ? p.accum[aidx] : make_float4(0, 0, 0, 0);
+                        need_path = true;
+                    }
+                }
+            }
+        }
+        // (3) camera ray for the next (frame, ray) of this lane's pixel (:514-542)
+        if (!done && lx >= 0 && need_path) {
+            if (r == 0) state = pt::seed(lx, y, p.frame_first + k);
+            float ax = 0.0f, ay = 0.0f;
+            if (!(p.flags & PT_FLAG_NO_AA)) {
+                ax = pt::random01(state);
+                ay = pt::random01(state);
+            }
+            float u = ((float)lx + ax) / (float)p.W - 0.5f;
+            float v = ((float)y + ay) / (float)p.H - 0.5f;
+            d = pt::normalize((cfwd + cright * u) + cup * v);
+            o = cpos;
+            inc = mk(0, 0, 0);
+            col = mk(1, 1, 1);
+            bounce = 0;
+            need_path = false;
+        }
+        bool busy = !done && lx >= 0 && !need_path;
+        if (__ballot(!done) == 0ull) break;
+        if (!busy) continue;
+
+        // (4) one segment: calculateRayCollision + the body of Trace's loop (:447-498)
+        bool fast = (bounce == 0 ? origin0_ok
+                                 : (p.scene_fast && in_guard(o.x, 0x1p-40f, 0x1p60f) &&
+                                    in_guard(o.y, 0x1p-40f, 0x1p60f) && in_guard(o.z, 0x1p-40f, 0x1p60f))) &&
+                    in_guard(d.x, 0x1p-20f, 2.0f) && d.x != 0.0f && in_guard(d.y, 0x1p-20f, 2.0f) && d.y != 0.0f &&
+                    in_guard(d.z, 0x1p-20f, 2.0f) && d.z != 0.0f;
+        f3 rd = mk(0, 0, 0);
+        if (fast) rd = mk(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
+        f3 normal = mk(0, 0, 0), hitp = mk(0, 0, 0);
+        int mat = 0;
+        bool hit = collide_v<COUNT>(S, p.sc.n_nodes, p.sc.n_spheres, p.flags, o, d, fast, rd, normal, hitp, mat, c);
+        if (COUNT) { c.seg++; if (hit) c.hits++; }
+        bool finished = false;
+        f3 rgb = inc;
+        if (hit && pt::length(col) > 0.01f) {
+            if (p.mode == 2) {
+                rgb = (normal + mk(1, 1, 1)) * 0.5f;
+                finished = true;
+            } else if (p.mode == 4) {
+                float s = pt::length(hitp - o);
+                float dist = 1.0f - pt::fsqrt(s + 1.0f) / (s + 1.0f);
+                float q = dist * dist;
+                rgb = mk(q, q, q);
+                finished = true;
+            } else {
+                o = hitp;
+                f3 diffuse = pt::normalize(normal + pt::random_unit_vector(state));
+                float kk = 2.0f * pt::dot(normal, d);
+                f3 specular = pt::normalize(d - normal * kk);
+                float4 m0 = S.mats[3 * mat], m1 = S.mats[3 * mat + 1], m2 = S.mats[3 * mat + 2];
+                if (p.mode == 3) {
+                    rgb = mk(m0.x, m0.y, m0.z);
+                    finished = true;
+                } else {
+                    float is_spec = (m1.w > pt::random01(state)) ? 1.0f : 0.0f;
+                    d = pt::mix(diffuse, specular, m0.w * is_spec);
+                    inc = inc + mk(m1.x, m1.y, m1.z) * col;
+                    col = col * pt::mix(mk(m0.x, m0.y, m0.z), mk(m2.x, m2.y, m2.z), is_spec);
+                    bounce++;
+                    if (bounce > p.max_bounce) {
+                        rgb = inc;
+                        finished = true;
+                    }
+                }
+            }
+        } else {
+            f3 env = mk(0, 0, 0);
+            if (!(p.flags & PT_FLAG_NO_SKY)) {
+                f3 dir = pt::normalize(d);
+                float tt = 0.5f * (dir.z + 1.0f);
+                float omt = 1.0f - tt;
+                env = mk(omt * 1.0f + tt * 0.5f, omt * 1.0f + tt * 0.7f, omt * 1.0f + tt * 1.0f);
+            }
+            rgb = inc + env * col;
+            finished = true;
+        }
+        if (finished) {
+            psum = psum + rgb;
+            r++;
+            if (r >= p.rpp) {
+                int f = p.frame_first + k;
+                acc = accumulate(acc, psum / (float)p.rpp, f, k > 0 || p.acc_first == 1);
+                psum = mk(0, 0, 0);
+                r = 0;
+                k++;
+            }
+            need_path = true;
+        }
+    }
+    flush_counters<COUNT>(p, c);
+}
+
 // ACES film tonemap epilogue (screenQuadFrag.c:12-26) -> RGBA8, alpha 255.
 __global__ __launch_bounds__(256) void k_aces(const float4* __restrict__ src, uchar4* __restrict__ dst,
                                               long long n) {
@@ -289,6 +572,8 @@ __global__ __launch_bounds__(256) void k_aces(const float4* __restrict__ src, uc
 }  // namespace
 
 // ===================================================================== host side
+constexpr size_t kLdsSceneMax = 48 * 1024;   // stage the scene in LDS up to 48 KiB
+
 struct pt_ctx {
     pt_config cfg{};
     int rows_local = 0;
@@ -302,7 +587,9 @@ struct pt_ctx {
     float4 *d_nodes = nullptr, *d_tris = nullptr, *d_mats = nullptr, *d_spheres = nullptr;
     unsigned long long* d_counters = nullptr;
     unsigned int* d_work = nullptr;
-    int n_nodes = 0, n_spheres = 0, n_mats = 0, n_slots = 0;
+    int n_nodes = 0, n_spheres = 0, n_mats = 0, n_slots = 0, scene_fast = 0;
+    size_t lds_bytes = 0;
+    unsigned persist_blocks = 2048;
     bool scene_ok = false, cam_ok = false, counting = false;
     float cam[12] = {0};
     int variant = 0;
@@ -357,6 +644,9 @@ int pt_create(const pt_config* cfg, pt_ctx** out) {
     HIPCHK(c, hipMalloc(&c->rgba8, std::max<size_t>(px, 1) * sizeof(uchar4)));
     HIPCHK(c, hipMalloc(&c->d_counters, 8 * sizeof(unsigned long long)));
     HIPCHK(c, hipMalloc(&c->d_work, 64));
+    int n_cu = 0;
+    HIPCHK(c, hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, cfg->device));
+    c->persist_blocks = (unsigned)std::max(1, n_cu) * 8u;   // 8 x 256 threads = 32 waves per CU
     // default camera (ogl_path_trace.h:53-54)
     const float defcam[12] = {0, -6, 1, 0, 0, 1, 0, 0, 0, 0, 0, 0};
     pt_set_camera(c, defcam);
@@ -495,6 +785,18 @@ int pt_upload_scene(pt_ctx* c, const float* tris, int n_tris, const float* bvh, 
     c->n_spheres = n_spheres;
     c->n_mats = n_mats;
     c->n_slots = 2 * n_leaves;
+    // exact-reciprocal slab guard, scene half: every box coordinate is 0
+    // or has magnitude in [2^-40, 2^60]
+    c->scene_fast = 1;
+    for (int i = 0; i < n_nodes && c->scene_fast; i++) {
+        const float* nd = bvh + 12 * (size_t)i;
+        for (int q = 0; q < 7; q++) {
+            if (q == 3) continue;
+            float a = std::fabs(nd[q]);
+            if (!(nd[q] == 0.0f || (a >= 0x1p-40f && a <= 0x1p60f))) { c->scene_fast = 0; break; }
+        }
+    }
+    c->lds_bytes = (size_t)(2 * n_nodes + 4 * c->n_slots + 3 * n_mats + 2 * n_spheres) * sizeof(float4);
     c->scene_ok = true;
     return PT_OK;
 }
@@ -521,7 +823,7 @@ int pt_set_counting(pt_ctx* c, int enable) {
 
 int pt_set_kernel(pt_ctx* c, int variant) {
     if (!c) return PT_E_ARG;
-    if (variant < 0 || variant > 0) return fail(c, PT_E_ARG, "unknown kernel variant");
+    if (variant < 0 || variant > 2) return fail(c, PT_E_ARG, "unknown kernel variant (0 wave+LDS, 1 tiled, 2 wave/global)");
     c->variant = variant;
     return PT_OK;
 }
@@ -557,9 +859,13 @@ int pt_render_async(pt_ctx* c, int frame_first, int n_frames, int acc_first) {
     p.rpp = c->cfg.rays_per_pixel;
     p.counters = c->d_counters;
     p.work_counter = c->d_work;
+    p.n_slots = c->n_slots;
+    p.n_mats = c->n_mats;
+    p.scene_fast = c->scene_fast;
     if (c->counting) HIPCHK(c, hipMemsetAsync(c->d_counters, 0, 8 * sizeof(unsigned long long), c->stream));
     if (c->rows_local == 0) return PT_OK;
-    dim3 grid((p.W + 15) / 16, (c->rows_local + 15) / 16);
+    bool use_lds = c->variant == 0 && c->lds_bytes <= kLdsSceneMax;
+    if (c->variant != 1) HIPCHK(c, hipMemsetAsync(c->d_work, 0, sizeof(unsigned), c->stream));
     hipEvent_t ev[2];
     for (int i = 0; i < 2; i++) {
         if (c->ev_free.empty()) {
@@ -571,10 +877,27 @@ int pt_render_async(pt_ctx* c, int frame_first, int n_frames, int acc_first) {
     }
     c->ev_pending.emplace_back(ev[0], ev[1]);
     HIPCHK(c, hipEventRecord(ev[0], c->stream));
-    if (c->counting)
-        hipLaunchKernelGGL(k_render_tiled<true>, grid, dim3(256), 0, c->stream, p);
-    else
-        hipLaunchKernelGGL(k_render_tiled<false>, grid, dim3(256), 0, c->stream, p);
+    if (c->variant == 1) {
+        dim3 grid((p.W + 15) / 16, (c->rows_local + 15) / 16);
+        if (c->counting)
+            hipLaunchKernelGGL(k_render_tiled<true>, grid, dim3(256), 0, c->stream, p);
+        else
+            hipLaunchKernelGGL(k_render_tiled<false>, grid, dim3(256), 0, c->stream, p);
+    } else {
+        // persistent grid: enough resident waves to fill every SIMD; surplus blocks find the
+        // queue empty and exit.  Never more blocks than 8x8 tiles (64 lanes per tile).
+        size_t lds = use_lds ? c->lds_bytes : 0;
+        unsigned tiles = (unsigned)(((p.W + 7) / 8) * ((c->rows_local + 7) / 8));
+        unsigned blocks = std::min<unsigned>(c->persist_blocks, std::max(1u, (tiles + 3) / 4));
+        dim3 grid(blocks);
+        if (use_lds) {
+            if (c->counting) hipLaunchKernelGGL((k_render_wave<true, true>), grid, dim3(256), lds, c->stream, p);
+            else hipLaunchKernelGGL((k_render_wave<false, true>), grid, dim3(256), lds, c->stream, p);
+        } else {
+            if (c->counting) hipLaunchKernelGGL((k_render_wave<true, false>), grid, dim3(256), 0, c->stream, p);
+            else hipLaunchKernelGGL((k_render_wave<false, false>), grid, dim3(256), 0, c->stream, p);
+        }
+    }
     HIPCHK(c, hipGetLastError());
     HIPCHK(c, hipEventRecord(ev[1], c->stream));
     c->count_pending = c->counting;

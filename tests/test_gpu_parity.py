@@ -11,6 +11,13 @@ import pt_host as H
 
 pytestmark = pytest.mark.gpu
 
+VARIANTS = [0, 1, 2]   # 0 persistent wave + LDS scene (default), 1 tiled, 2 persistent, global scene
+
+
+@pytest.fixture(params=VARIANTS, ids=lambda v: "v%d" % v)
+def V(request):
+    return request.param
+
 
 def bits(a):
     return np.ascontiguousarray(a, np.float32).view(np.uint32)
@@ -40,37 +47,38 @@ def gpu_render(sc, W, H_, max_bounce=5, mode=1, frame_first=1, n_frames=1, acc_f
 
 
 @pytest.mark.parametrize("mode", [2, 3, 4])
-def test_debug_modes_bitwise(cornell_scene, mode):
+def test_debug_modes_bitwise(cornell_scene, mode, V):
     want = O.render(cornell_scene, 64, 48, mode=mode)
-    got = gpu_render(cornell_scene, 64, 48, mode=mode)
+    got = gpu_render(cornell_scene, 64, 48, mode=mode, variant=V)
     assert_bitwise(got, want, "mode %d" % mode)
 
 
 @pytest.mark.parametrize("spp", [1, 4, 16])
-def test_shaded_cornell_bitwise(cornell_scene, spp):
+def test_shaded_cornell_bitwise(cornell_scene, spp, V):
     want = O.render(cornell_scene, 64, 64, max_bounce=5, n_frames=spp)
-    got = gpu_render(cornell_scene, 64, 64, max_bounce=5, n_frames=spp)
+    got = gpu_render(cornell_scene, 64, 64, max_bounce=5, n_frames=spp, variant=V)
     assert_bitwise(got, want, "cornell %d spp" % spp)
 
 
-def test_shaded_ship_bitwise(ship_scene):
+def test_shaded_ship_bitwise(ship_scene, V):
     want = O.render(ship_scene, 80, 60, max_bounce=5, n_frames=4)
-    got = gpu_render(ship_scene, 80, 60, max_bounce=5, n_frames=4)
+    got = gpu_render(ship_scene, 80, 60, max_bounce=5, n_frames=4, variant=V)
     assert_bitwise(got, want, "ship")
 
 
-def test_eight_bounces_and_frame_offset(cornell_scene):
+def test_eight_bounces_and_frame_offset(cornell_scene, V):
     # frames 3000..3002 exercise the signed-overflow seed term (frame*719393 > 2^31)
     prior = np.random.default_rng(1).random((36, 64, 4), dtype=np.float32)
     want = O.render(cornell_scene, 64, 36, max_bounce=8, frame_first=3000, n_frames=3, acc_first=1,
                     accum=prior.copy())
     got = gpu_render(cornell_scene, 64, 36, max_bounce=8, frame_first=3000, n_frames=3, acc_first=1,
-                     prior=prior)
+                     prior=prior, variant=V)
     assert_bitwise(got, want, "8 bounces")
 
 
-def test_fused_equals_separate_dispatches(cornell_scene):
+def test_fused_equals_separate_dispatches(cornell_scene, V):
     pt = H.PathTracer(48, 32, max_bounce=8)
+    pt.set_kernel(V)
     pt.upload(cornell_scene)
     for f in range(1, 6):
         pt.dispatch(f, 0 if f == 1 else 1)
@@ -83,39 +91,40 @@ def test_fused_equals_separate_dispatches(cornell_scene):
 
 @pytest.mark.parametrize("flags", [H.PT_FLAG_NO_AA, H.PT_FLAG_NO_SKY, H.PT_FLAG_NO_SPHERES,
                                    H.PT_FLAG_NO_TRIANGLES])
-def test_toggles_bitwise(cornell_scene, flags):
+def test_toggles_bitwise(cornell_scene, flags, V):
     want = O.render(cornell_scene, 40, 30, n_frames=2, flags=flags)
-    got = gpu_render(cornell_scene, 40, 30, n_frames=2, flags=flags)
+    got = gpu_render(cornell_scene, 40, 30, n_frames=2, flags=flags, variant=V)
     assert_bitwise(got, want, "flags %d" % flags)
 
 
-def test_ref_dispatch_footprint(cornell_scene):
+def test_ref_dispatch_footprint(cornell_scene, V):
     # glDispatchCompute(W/10, H/10) with 10x10 groups writes only the 250x250 block at 256^2
-    got = gpu_render(cornell_scene, 256, 256, mode=2, flags=H.PT_FLAG_REF_DISPATCH)
+    got = gpu_render(cornell_scene, 256, 256, mode=2, flags=H.PT_FLAG_REF_DISPATCH, variant=V)
     assert np.all(got[250:] == 0) and np.all(got[:, 250:] == 0)
     want = O.render(cornell_scene, 256, 256, mode=2)
     assert_bitwise(got[:250, :250], want[:250, :250], "footprint")
 
 
-def test_partition_invariance(cornell_scene):
-    full = gpu_render(cornell_scene, 64, 50, max_bounce=8, n_frames=3)
-    parts = [gpu_render(cornell_scene, 64, 50, max_bounce=8, n_frames=3, rank=r, world=3) for r in range(3)]
+def test_partition_invariance(cornell_scene, V):
+    full = gpu_render(cornell_scene, 64, 50, max_bounce=8, n_frames=3, variant=V)
+    parts = [gpu_render(cornell_scene, 64, 50, max_bounce=8, n_frames=3, rank=r, world=3, variant=V)
+             for r in range(3)]
     assert_bitwise(H.assemble_rows(parts, 50), full, "3-way row split")
 
 
-def test_counters_match_oracle(cornell_scene):
+def test_counters_match_oracle(cornell_scene, V):
     want_img, want_cnt = O.render(cornell_scene, 48, 48, max_bounce=8, n_frames=4, counters=True)
-    got_img, (ms, cnt) = gpu_render(cornell_scene, 48, 48, max_bounce=8, n_frames=4, counting=True)
+    got_img, (ms, cnt) = gpu_render(cornell_scene, 48, 48, max_bounce=8, n_frames=4, counting=True, variant=V)
     assert_bitwise(got_img, want_img, "counting build")
     assert [cnt["segments"], cnt["node_visits"], cnt["tri_tests"], cnt["sphere_tests"], cnt["hits"]] == \
         [int(x) for x in want_cnt]
 
 
-def test_full_hd_sampled_pixels(cornell_scene):
+def test_full_hd_sampled_pixels(cornell_scene, V):
     """1920x1080, 8 bounces, 2 spp: the full-size GPU frame checked bit-exactly at 4000
     oracle-rendered pixels (plus every pixel of the first and last rows)."""
     W, Hh = 1920, 1080
-    got = gpu_render(cornell_scene, W, Hh, max_bounce=8, n_frames=2)
+    got = gpu_render(cornell_scene, W, Hh, max_bounce=8, n_frames=2, variant=V)
     rng = np.random.default_rng(7)
     xs = np.concatenate([rng.integers(0, W, 4000), np.arange(W), np.arange(W)])
     ys = np.concatenate([rng.integers(0, Hh, 4000), np.zeros(W, int), np.full(W, Hh - 1)])
@@ -123,15 +132,29 @@ def test_full_hd_sampled_pixels(cornell_scene):
     assert_bitwise(got[ys, xs], want, "1080p samples")
 
 
-def test_golden_fixtures(cornell_scene, ship_scene):
+def test_golden_fixtures(cornell_scene, ship_scene, V):
     """Committed fixtures (oracle == numpy twin, tests/golden/make_golden.py)."""
     import os
     z = np.load(os.path.join(os.path.dirname(__file__), "golden", "golden_images.npz"))
     for key in z.files:
         scene, W, Hh, mb, mode, spp = key.split("_")
         sc = cornell_scene if scene == "cornell" else ship_scene
-        got = gpu_render(sc, int(W), int(Hh), max_bounce=int(mb), mode=int(mode), n_frames=int(spp))
+        got = gpu_render(sc, int(W), int(Hh), max_bounce=int(mb), mode=int(mode), n_frames=int(spp), variant=V)
         assert_bitwise(got, z[key], key)
+
+
+def test_exact_reciprocal_guard_fallback(cornell_scene, V):
+    """Scene scaled by 2^-100: box coordinates fall outside the exact-reciprocal guard, so
+    every slab test takes the IEEE-division chain; results must still be bit-exact."""
+    sc = {k: np.array(v, copy=True) for k, v in cornell_scene.items()}
+    s = np.float32(2.0 ** -100)
+    sc["tris"][:, [0, 1, 2, 4, 5, 6, 8, 9, 10]] *= s
+    sc["nodes"][:, [0, 1, 2, 4, 5, 6]] *= s
+    sc["spheres"][:, :4] *= s
+    sc["cam"][:3] *= s
+    want = O.render(sc, 40, 30, max_bounce=5, n_frames=2)
+    got = gpu_render(sc, 40, 30, max_bounce=5, n_frames=2, variant=V)
+    assert_bitwise(got, want, "scaled scene")
 
 
 def test_aces_epilogue(cornell_scene):

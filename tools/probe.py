@@ -1,0 +1,59 @@
+"""Quick A/B of kernel variants / launch shapes on one GPU (interleaved, one process).
+
+python tools/probe.py --spp 64 --variants 0,1,2 --chunks 16,64 --rounds 2
+Prints Mrays/s and kernel ms per configuration; segment counts come from a counting pass.
+"""
+import argparse
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(REPO, "opengl-path-tracing_amd"))
+
+import pt_host  # noqa: E402
+import pt_scenes  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--spp", type=int, default=64)
+    ap.add_argument("--variants", default="0,1,2")
+    ap.add_argument("--chunks", default="64")
+    ap.add_argument("--rounds", type=int, default=2)
+    ap.add_argument("--scene", default="cornell")
+    ap.add_argument("--width", type=int, default=1920)
+    ap.add_argument("--height", type=int, default=1080)
+    ap.add_argument("--bounces", type=int, default=8)
+    a = ap.parse_args()
+    sb = pt_host.setupBuffers(*pt_scenes.write_scene(a.scene, os.path.join(REPO, "scenes")))
+    pt = pt_host.PathTracer(a.width, a.height, max_bounce=a.bounces)
+    pt.upload(sb)
+    seg = {}
+    configs = [(int(v), int(c)) for v in a.variants.split(",") for c in a.chunks.split(",")]
+    for v, c in configs:
+        pt.set_kernel(v)
+        pt.set_counting(True)
+        total = 0
+        for f0 in range(1, a.spp + 1, c):
+            pt.render(f0, min(c, a.spp - f0 + 1), 0 if f0 == 1 else 1)
+            total += pt.stats()[1]["segments"]
+        pt.set_counting(False)
+        seg[(v, c)] = total
+    for rnd in range(a.rounds):
+        for v, c in configs:
+            pt.set_kernel(v)
+            pt.timing(reset=True)
+            t0 = time.perf_counter()
+            for f0 in range(1, a.spp + 1, c):
+                pt.render_async(f0, min(c, a.spp - f0 + 1), 0 if f0 == 1 else 1)
+            pt.sync()
+            dt = time.perf_counter() - t0
+            kms, n = pt.timing(reset=True)
+            print("round %d variant %d chunk %4d: %8.1f Mrays/s  wall %.1f ms  kernel %.1f ms (%d launches)  %.3f ms/frame"
+                  % (rnd, v, c, seg[(v, c)] / dt / 1e6, dt * 1e3, kms, n, dt * 1e3 / a.spp), flush=True)
+    pt.close()
+
+
+if __name__ == "__main__":
+    main()
