@@ -384,6 +384,97 @@ __device__ __forceinline__ bool collide_v(const SceneView& S, int n_nodes, int n
     return hit;
 }
 
+// hit_triangle without early exits: every lane evaluates the full test and the verdict is
+// a select, so a wave does the test once instead of once per divergent exit path.
+// Same operations, same bits as tri_hit().
+__device__ __forceinline__ float tri_hit_bf(const float4* T, f3 o, f3 d, float tbest, f3& n) {
+    float4 q0 = T[0], q1 = T[1], q2 = T[2], q3 = T[3];
+    n = mk(q0.w, q1.w, q2.w);
+    float t = -(pt::dot(n, o) + q3.x) / pt::dot(n, d);
+    f3 v0 = mk(q0.x, q0.y, q0.z), v1 = mk(q1.x, q1.y, q1.z), v2 = mk(q2.x, q2.y, q2.z);
+    f3 p = o + d * t;
+    float e0 = pt::dot(n, pt::cross(v1 - v0, p - v0));
+    float e1 = pt::dot(n, pt::cross(v2 - v1, p - v1));
+    float e2 = pt::dot(n, pt::cross(v0 - v2, p - v2));
+    bool ok = !(t < 0.0f) && (t < tbest) && (e0 > 0.0f) && (e1 > 0.0f) && (e2 > 0.0f);
+    return ok ? t : -1.0f;
+}
+
+// calculateRayCollision with "while-while" scheduling of the stackless walk: each lane
+// advances through the link chain until it reaches a leaf whose box it hits (or the walk
+// ends), and only then do the lanes that stopped at leaves run the two triangle tests
+// together.  Each lane still visits exactly the reference's node sequence and tests each
+// leaf before its next node, with the same t -- only the interleaving across lanes changes.
+template <bool COUNT>
+__device__ __forceinline__ bool collide_ww(const SceneView& S, int n_nodes, int n_spheres, int flags,
+                                           bool active, f3 o, f3 d, bool fast, f3 rd, f3& normal,
+                                           f3& hitp, int& mat, Cnt& c) {
+    float t = __builtin_huge_valf();
+    bool hit = false;
+    if (active && !(flags & PT_FLAG_NO_SPHERES)) {
+        for (int si = 0; si < n_spheres; si++) {
+            float4 s0 = S.spheres[2 * si];
+            f3 cc = mk(s0.x, s0.y, s0.z);
+            f3 oc = o - cc;
+            float a = pt::dot(d, d);
+            float half_b = pt::dot(oc, d);
+            float cq = pt::dot(oc, oc) - s0.w;
+            float disc = half_b * half_b - a * cq;
+            float ht = disc < 0.0f ? -1.0f : (-half_b - pt::fsqrt(disc)) / a;
+            if (COUNT) c.sph++;
+            if (ht > 0.0001f && ht < t) {
+                f3 pn = pt::normalize((o + d * ht) - cc);
+                if (pt::dot(pn, d) > 0.0f) pn = pn * -1.0f;
+                hit = true;
+                t = ht;
+                normal = pn;
+                hitp = o + d * ht;
+                mat = __float_as_int(S.spheres[2 * si + 1].x);
+            }
+        }
+    }
+    int bi = (active && !(flags & PT_FLAG_NO_TRIANGLES) && n_nodes > 0) ? 0 : -1;
+    int steps = 0;
+    int leaf = 0;
+    bool pend = false;
+    for (;;) {
+        while (bi > -1 && !pend && steps < n_nodes) {
+            float4 lo = S.nodes[2 * bi], hi = S.nodes[2 * bi + 1];
+            int a = __float_as_int(lo.w), b = __float_as_int(hi.w);
+            bool hb = fast ? slab_fast(lo, hi, o, d, rd, t) : slab(lo, hi, o, d, t);
+            if (COUNT) c.nodes++;
+            steps++;
+            if (hb && a < 0) {
+                pend = true;
+                leaf = ~a;
+            }
+            bi = (hb && a >= 0) ? a : b;
+        }
+        if (!__any(pend)) break;
+        if (pend) {
+            if (COUNT) c.tri += 2;
+            const float4* T0 = S.tris + 8 * (leaf >> 1);
+            f3 n0, n1;
+            float h1 = tri_hit_bf(T0, o, d, t, n0);
+            float h2 = tri_hit_bf(T0 + 4, o, d, t, n1);   // single-tri leaves hold a copy
+            bool c1 = h1 > 0.0001f && h1 < t && (h1 < h2 || h2 < 0.0001f);
+            bool c2 = !c1 && h2 > 0.0001f && h2 < t;
+            if (c1 || c2) {
+                f3 nn = c1 ? n0 : n1;
+                float th = c1 ? h1 : h2;
+                if (pt::dot(nn, d) > 0.0f) nn = nn * -1.0f;
+                hit = true;
+                t = th;
+                normal = nn;
+                hitp = o + d * th;
+                mat = __float_as_int(T0[c1 ? 3 : 7].y);
+            }
+            pend = false;
+        }
+    }
+    return hit;
+}
+
 template <bool COUNT, bool LDS>
 __global__ __launch_bounds__(256) void k_render_wave(KParams p) {
     extern __shared__ float4 lds[];
@@ -477,7 +568,7 @@ __global__ __launch_bounds__(256) void k_render_wave(KParams p) {
         }
         bool busy = !done && lx >= 0 && !need_path;
         if (__ballot(!done) == 0ull) break;
-        if (!busy) continue;
+        if (!__any(busy)) continue;
 
         // (4) one segment: calculateRayCollision + the body of Trace's loop (:447-498)
         bool fast = (bounce == 0 ? origin0_ok
@@ -489,7 +580,9 @@ __global__ __launch_bounds__(256) void k_render_wave(KParams p) {
         if (fast) rd = mk(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
         f3 normal = mk(0, 0, 0), hitp = mk(0, 0, 0);
         int mat = 0;
-        bool hit = collide_v<COUNT>(S, p.sc.n_nodes, p.sc.n_spheres, p.flags, o, d, fast, rd, normal, hitp, mat, c);
+        bool hit = collide_ww<COUNT>(S, p.sc.n_nodes, p.sc.n_spheres, p.flags, busy, o, d, fast, rd, normal,
+                                     hitp, mat, c);
+        if (!busy) continue;
         if (COUNT) { c.seg++; if (hit) c.hits++; }
         bool finished = false;
         f3 rgb = inc;

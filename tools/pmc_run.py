@@ -1,0 +1,30 @@
+"""Workload for PMC passes: the bench configuration's render kernel, one warm-up launch and
+`--launches` measured launches of `--chunk` frames (C2: Cornell 1920x1080, 8 bounces).
+Run under rocprofv3 --pmc ... -- python3 tools/pmc_run.py; tools/pmc_traffic.py reduces."""
+import argparse
+import os
+import sys
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(REPO, "opengl-path-tracing_amd"))
+
+import pt_host  # noqa: E402
+import pt_scenes  # noqa: E402
+
+ap = argparse.ArgumentParser()
+ap.add_argument("--chunk", type=int, default=64)
+ap.add_argument("--launches", type=int, default=2)
+ap.add_argument("--variant", type=int, default=0)
+ap.add_argument("--scene", default="cornell")
+ap.add_argument("--width", type=int, default=1920)
+ap.add_argument("--height", type=int, default=1080)
+a = ap.parse_args()
+sb = pt_host.setupBuffers(*pt_scenes.write_scene(a.scene, os.path.join(REPO, "scenes")))
+pt = pt_host.PathTracer(a.width, a.height, max_bounce=8)
+pt.set_kernel(a.variant)
+pt.upload(sb)
+pt.render(1, a.chunk, 0)
+for i in range(a.launches):
+    pt.render(1 + a.chunk * (i + 1), a.chunk, 1)
+pt.close()
+print("pmc workload done")
