@@ -94,12 +94,21 @@ int pt_stream(pt_ctx* ctx, void** stream);
  * out[0] segments, [1] node visits, [2] triangle tests, [3] sphere tests, [4] hits. */
 int pt_set_counting(pt_ctx* ctx, int enable);
 int pt_stats(pt_ctx* ctx, double* kernel_ms, unsigned long long out[5]);
+/* Counting-build diagnostics of the last render: out[0..4] as pt_stats, then per kernel
+ * phase (traversal step, leaf test, segment) the wave iterations and the active lanes
+ * summed over them: [5] trav waves, [6] trav lanes, [7] leaf waves, [8] leaf lanes,
+ * [9] segment waves, [10] segment lanes (persistent kernels; 0 for the tiled kernel). */
+int pt_stats_ex(pt_ctx* ctx, unsigned long long out[16]);
 /* Sum of render-kernel durations (HIP events on the render stream) and the number of
  * launches since the last reset; reset != 0 clears both after reading. */
 int pt_timing(pt_ctx* ctx, double* total_kernel_ms, int* n_launches, int reset);
 
 /* Kernel variant selection (0 = default/fastest); see DESIGN.md §5 for the list. */
 int pt_set_kernel(pt_ctx* ctx, int variant);
+/* Wave-scheduling thresholds of the state-machine kernel (lanes, 1..64):
+ * key 0 = run the leaf phase once this many lanes wait at leaves,
+ * key 1 = run the shading phase once this many lanes finished their segment. */
+int pt_set_tuning(pt_ctx* ctx, int key, int value);
 
 #ifdef __cplusplus
 }

@@ -50,11 +50,25 @@ struct KParams {
     unsigned int* work_counter;    // persistent kernel pixel queue
     int n_slots, n_mats;           // triangle slots / materials (LDS staging sizes)
     int scene_fast;                // every box coordinate inside the exact-reciprocal guard
+    int leaf_thresh, shade_thresh; // wave scheduling thresholds of the state-machine kernel
 };
 
 struct Cnt {
     uint32_t seg, nodes, tri, sph, hits;
+    // counting-build diagnostics: per phase, wave iterations (counted once per wave by the
+    // first active lane) and active lanes summed over those iterations
+    uint32_t tw, tl, lw, ll, sw, sl;
 };
+constexpr int kNumCounters = 11;
+
+// Records one wave iteration of a phase: the first active lane adds 1 and popcount(exec).
+__device__ __forceinline__ void diag_tick(uint32_t& waves, uint32_t& lanes) {
+    unsigned long long e = __builtin_amdgcn_read_exec();
+    if ((int)(threadIdx.x & 63) == __ffsll((long long)e) - 1) {
+        waves++;
+        lanes += (uint32_t)__popcll(e);
+    }
+}
 
 // ------------------------------------------------------------------ intersection
 // bvh_intersect (computeShader.c:309-365): the exact division/compare chain; NaN compares
@@ -240,8 +254,8 @@ __device__ __forceinline__ unsigned long long wave_sum(unsigned long long v) {
 template <bool COUNT>
 __device__ __forceinline__ void flush_counters(const KParams& p, const Cnt& c) {
     if (!COUNT) return;
-    unsigned long long v[5] = {c.seg, c.nodes, c.tri, c.sph, c.hits};
-    for (int i = 0; i < 5; i++) {
+    unsigned long long v[kNumCounters] = {c.seg, c.nodes, c.tri, c.sph, c.hits, c.tw, c.tl, c.lw, c.ll, c.sw, c.sl};
+    for (int i = 0; i < kNumCounters; i++) {
         unsigned long long s = wave_sum(v[i]);
         if ((threadIdx.x & 63) == 0) atomicAdd(&p.counters[i], s);
     }
@@ -442,7 +456,7 @@ __device__ __forceinline__ bool collide_ww(const SceneView& S, int n_nodes, int 
             float4 lo = S.nodes[2 * bi], hi = S.nodes[2 * bi + 1];
             int a = __float_as_int(lo.w), b = __float_as_int(hi.w);
             bool hb = fast ? slab_fast(lo, hi, o, d, rd, t) : slab(lo, hi, o, d, t);
-            if (COUNT) c.nodes++;
+            if (COUNT) { c.nodes++; diag_tick(c.tw, c.tl); }
             steps++;
             if (hb && a < 0) {
                 pend = true;
@@ -452,7 +466,7 @@ __device__ __forceinline__ bool collide_ww(const SceneView& S, int n_nodes, int 
         }
         if (!__any(pend)) break;
         if (pend) {
-            if (COUNT) c.tri += 2;
+            if (COUNT) { c.tri += 2; diag_tick(c.lw, c.ll); }
             const float4* T0 = S.tris + 8 * (leaf >> 1);
             f3 n0, n1;
             float h1 = tri_hit_bf(T0, o, d, t, n0);
@@ -475,8 +489,8 @@ __device__ __forceinline__ bool collide_ww(const SceneView& S, int n_nodes, int 
     return hit;
 }
 
-template <bool COUNT, bool LDS>
-__global__ __launch_bounds__(256) void k_render_wave(KParams p) {
+template <bool COUNT, bool LDS, int MINW>
+__global__ __launch_bounds__(256, MINW) void k_render_wave(KParams p) {
     extern __shared__ float4 lds[];
     SceneView S;
     if (LDS) {
@@ -583,7 +597,7 @@ __global__ __launch_bounds__(256) void k_render_wave(KParams p) {
         bool hit = collide_ww<COUNT>(S, p.sc.n_nodes, p.sc.n_spheres, p.flags, busy, o, d, fast, rd, normal,
                                      hitp, mat, c);
         if (!busy) continue;
-        if (COUNT) { c.seg++; if (hit) c.hits++; }
+        if (COUNT) { c.seg++; if (hit) c.hits++; diag_tick(c.sw, c.sl); }
         bool finished = false;
         f3 rgb = inc;
         if (hit && pt::length(col) > 0.01f) {
@@ -644,6 +658,266 @@ __global__ __launch_bounds__(256) void k_render_wave(KParams p) {
     flush_counters<COUNT>(p, c);
 }
 
+// =====================================================================================
+// Variant 6: persistent state-machine kernel.  Every lane carries one path through three
+// states -- TRAV (walking the link chain), LEAF (stopped at a leaf whose box it hit), SHADE
+// (segment finished: shade / regenerate / set up the next segment) -- and each wave
+// iteration runs ONE phase for the lanes in that state, picked by ballot counts:
+//   SHADE when >= shade_thresh lanes wait to shade (or nothing else is runnable),
+//   LEAF  when >= leaf_thresh lanes wait at leaves (or no lane is walking),
+//   TRAV  otherwise (an inner walk loop that yields when either threshold is reached).
+// A lane's own operation sequence is exactly the reference's (node, leaf tests before the
+// next node, same t), so results are bit-identical; only lane interleaving changes.
+// =====================================================================================
+enum : int { ST_DONE = 0, ST_TRAV = 1, ST_LEAF = 2, ST_SHADE = 3 };
+
+template <bool COUNT, bool LDS>
+__global__ __launch_bounds__(256) void k_render_sm(KParams p) {
+    extern __shared__ float4 lds[];
+    SceneView S;
+    if (LDS) {
+        int nn = 2 * p.sc.n_nodes, nt = 4 * p.n_slots, nm = 3 * p.n_mats, ns = 2 * p.sc.n_spheres;
+        for (int i = threadIdx.x; i < nn; i += blockDim.x) lds[i] = p.sc.nodes[i];
+        for (int i = threadIdx.x; i < nt; i += blockDim.x) lds[nn + i] = p.sc.tris[i];
+        for (int i = threadIdx.x; i < nm; i += blockDim.x) lds[nn + nt + i] = p.sc.mats[i];
+        for (int i = threadIdx.x; i < ns; i += blockDim.x) lds[nn + nt + nm + i] = p.sc.spheres[i];
+        __syncthreads();
+        S.nodes = lds;
+        S.tris = lds + nn;
+        S.mats = lds + nn + nt;
+        S.spheres = lds + nn + nt + nm;
+    } else {
+        S.nodes = p.sc.nodes;
+        S.tris = p.sc.tris;
+        S.mats = p.sc.mats;
+        S.spheres = p.sc.spheres;
+    }
+    const int lane = threadIdx.x & 63;
+    const f3 cpos = mk(p.cam[0], p.cam[1], p.cam[2]), cfwd = mk(p.cam[3], p.cam[4], p.cam[5]);
+    const f3 cright = mk(p.cam[6], p.cam[7], p.cam[8]), cup = mk(p.cam[9], p.cam[10], p.cam[11]);
+    const int tiles_x = (p.W + 7) >> 3;
+    const unsigned total_ids = (unsigned)tiles_x * (unsigned)((p.rows_local + 7) >> 3) * 64u;
+    const int n_nodes = p.sc.n_nodes;
+    const bool use_tris = !(p.flags & PT_FLAG_NO_TRIANGLES) && n_nodes > 0;
+
+    Cnt c = {0, 0, 0, 0, 0};
+    int st = ST_SHADE;
+    bool fresh = true;        // SHADE without a finished segment (start / after fetch)
+    bool need_ray = true;     // next SHADE must start a new camera ray
+    int lx = -1, y = 0;
+    size_t aidx = 0;
+    int k = 0, r = 0, bounce = 0;
+    float4 acc = make_float4(0, 0, 0, 0);
+    f3 psum = mk(0, 0, 0), o = mk(0, 0, 0), d = mk(0, 0, 1), inc = mk(0, 0, 0), col = mk(1, 1, 1);
+    uint32_t state = 0;
+    // segment state
+    bool fast = false, hit = false;
+    f3 rd = mk(0, 0, 0), normal = mk(0, 0, 0), hitp = mk(0, 0, 0);
+    float t = 0.0f;
+    int mat = 0, bi = -1, leaf = 0, steps = 0;
+
+    for (;;) {
+        int nS = __popcll(__ballot(st == ST_SHADE));
+        int nL = __popcll(__ballot(st == ST_LEAF));
+        int nT = __popcll(__ballot(st == ST_TRAV));
+        if (nS + nL + nT == 0) break;
+        if (nS > 0 && (nS >= p.shade_thresh || (nT == 0 && nL == 0))) {
+            // ---------------- SHADE: finish segment, regenerate, set up next segment
+            if (st == ST_SHADE && !fresh) {
+                if (COUNT) { c.seg++; if (hit) c.hits++; diag_tick(c.sw, c.sl); }
+                bool finished = false;
+                f3 rgb = inc;
+                if (hit && pt::length(col) > 0.01f) {
+                    if (p.mode == 2) {
+                        rgb = (normal + mk(1, 1, 1)) * 0.5f;
+                        finished = true;
+                    } else if (p.mode == 4) {
+                        float s = pt::length(hitp - o);
+                        float dist = 1.0f - pt::fsqrt(s + 1.0f) / (s + 1.0f);
+                        float q = dist * dist;
+                        rgb = mk(q, q, q);
+                        finished = true;
+                    } else {
+                        o = hitp;
+                        f3 diffuse = pt::normalize(normal + pt::random_unit_vector(state));
+                        float kk = 2.0f * pt::dot(normal, d);
+                        f3 specular = pt::normalize(d - normal * kk);
+                        float4 m0 = S.mats[3 * mat], m1 = S.mats[3 * mat + 1], m2 = S.mats[3 * mat + 2];
+                        if (p.mode == 3) {
+                            rgb = mk(m0.x, m0.y, m0.z);
+                            finished = true;
+                        } else {
+                            float is_spec = (m1.w > pt::random01(state)) ? 1.0f : 0.0f;
+                            d = pt::mix(diffuse, specular, m0.w * is_spec);
+                            inc = inc + mk(m1.x, m1.y, m1.z) * col;
+                            col = col * pt::mix(mk(m0.x, m0.y, m0.z), mk(m2.x, m2.y, m2.z), is_spec);
+                            bounce++;
+                            if (bounce > p.max_bounce) {
+                                rgb = inc;
+                                finished = true;
+                            }
+                        }
+                    }
+                } else {
+                    f3 env = mk(0, 0, 0);
+                    if (!(p.flags & PT_FLAG_NO_SKY)) {
+                        f3 dir = pt::normalize(d);
+                        float tt = 0.5f * (dir.z + 1.0f);
+                        float omt = 1.0f - tt;
+                        env = mk(omt * 1.0f + tt * 0.5f, omt * 1.0f + tt * 0.7f, omt * 1.0f + tt * 1.0f);
+                    }
+                    rgb = inc + env * col;
+                    finished = true;
+                }
+                need_ray = finished;
+                if (finished) {
+                    psum = psum + rgb;
+                    r++;
+                    if (r >= p.rpp) {
+                        int f = p.frame_first + k;
+                        acc = accumulate(acc, psum / (float)p.rpp, f, k > 0 || p.acc_first == 1);
+                        psum = mk(0, 0, 0);
+                        r = 0;
+                        k++;
+                    }
+                }
+                fresh = true;
+            }
+            if (st == ST_SHADE && need_ray && lx >= 0 && k >= p.n_frames) {
+                p.accum[aidx] = acc;
+                lx = -1;
+            }
+            // wave-aggregated pull from the pixel queue
+            bool want = st == ST_SHADE && lx < 0;
+            unsigned long long m = __ballot(want);
+            if (m) {
+                int leader = __ffsll((long long)m) - 1;
+                unsigned base = 0;
+                if (lane == leader) base = atomicAdd(p.work_counter, (unsigned)__popcll(m));
+                base = __shfl(base, leader, 64);
+                if (want) {
+                    unsigned id = base + (unsigned)__popcll(m & ((1ull << lane) - 1ull));
+                    if (id >= total_ids) {
+                        st = ST_DONE;
+                    } else {
+                        unsigned tile = id >> 6, w = id & 63u;
+                        int cx = (int)(tile % (unsigned)tiles_x) * 8 + (int)(w & 7u);
+                        int crow = (int)(tile / (unsigned)tiles_x) * 8 + (int)(w >> 3);
+                        int cy = p.row0 + crow * p.row_stride;
+                        if (cx < p.W && crow < p.rows_local && cx < p.x_limit && cy < p.y_limit) {
+                            lx = cx;
+                            y = cy;
+                            aidx = (size_t)crow * p.W + cx;
+                            k = 0;
+                            r = 0;
+                            psum = mk(0, 0, 0);
+                            acc = p.acc_first ? p.accum[aidx] : make_float4(0, 0, 0, 0);
+                            need_ray = true;
+                        }
+                    }
+                }
+            }
+            if (st == ST_SHADE && lx >= 0) {
+                if (need_ray) {       // camera ray (:514-542)
+                    if (r == 0) state = pt::seed(lx, y, p.frame_first + k);
+                    float ax = 0.0f, ay = 0.0f;
+                    if (!(p.flags & PT_FLAG_NO_AA)) {
+                        ax = pt::random01(state);
+                        ay = pt::random01(state);
+                    }
+                    float u = ((float)lx + ax) / (float)p.W - 0.5f;
+                    float v = ((float)y + ay) / (float)p.H - 0.5f;
+                    d = pt::normalize((cfwd + cright * u) + cup * v);
+                    o = cpos;
+                    inc = mk(0, 0, 0);
+                    col = mk(1, 1, 1);
+                    bounce = 0;
+                    need_ray = false;
+                }
+                // segment set-up: exact-reciprocal guard, spheres (:372-385), walk start
+                fast = p.scene_fast && in_guard(o.x, 0x1p-40f, 0x1p60f) && in_guard(o.y, 0x1p-40f, 0x1p60f) &&
+                       in_guard(o.z, 0x1p-40f, 0x1p60f) && in_guard(d.x, 0x1p-20f, 2.0f) && d.x != 0.0f &&
+                       in_guard(d.y, 0x1p-20f, 2.0f) && d.y != 0.0f && in_guard(d.z, 0x1p-20f, 2.0f) && d.z != 0.0f;
+                if (fast) rd = mk(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
+                t = __builtin_huge_valf();
+                hit = false;
+                if (!(p.flags & PT_FLAG_NO_SPHERES)) {
+                    for (int si = 0; si < p.sc.n_spheres; si++) {
+                        float4 s0 = S.spheres[2 * si];
+                        f3 cc = mk(s0.x, s0.y, s0.z);
+                        f3 oc = o - cc;
+                        float a = pt::dot(d, d);
+                        float half_b = pt::dot(oc, d);
+                        float cq = pt::dot(oc, oc) - s0.w;
+                        float disc = half_b * half_b - a * cq;
+                        float ht = disc < 0.0f ? -1.0f : (-half_b - pt::fsqrt(disc)) / a;
+                        if (COUNT) c.sph++;
+                        if (ht > 0.0001f && ht < t) {
+                            f3 pn = pt::normalize((o + d * ht) - cc);
+                            if (pt::dot(pn, d) > 0.0f) pn = pn * -1.0f;
+                            hit = true;
+                            t = ht;
+                            normal = pn;
+                            hitp = o + d * ht;
+                            mat = __float_as_int(S.spheres[2 * si + 1].x);
+                        }
+                    }
+                }
+                fresh = false;
+                steps = 0;
+                bi = use_tris ? 0 : -1;
+                st = use_tris ? ST_TRAV : ST_SHADE;
+            }
+        } else if (nL > 0 && (nL >= p.leaf_thresh || nT == 0)) {
+            // ---------------- LEAF: both triangle tests + the 2-way choice (:406-429)
+            if (st == ST_LEAF) {
+                if (COUNT) { c.tri += 2; diag_tick(c.lw, c.ll); }
+                const float4* T0 = S.tris + 8 * (leaf >> 1);
+                f3 n0, n1;
+                float h1 = tri_hit_bf(T0, o, d, t, n0);
+                float h2 = tri_hit_bf(T0 + 4, o, d, t, n1);
+                bool c1 = h1 > 0.0001f && h1 < t && (h1 < h2 || h2 < 0.0001f);
+                bool c2 = !c1 && h2 > 0.0001f && h2 < t;
+                if (c1 || c2) {
+                    f3 nn = c1 ? n0 : n1;
+                    float th = c1 ? h1 : h2;
+                    if (pt::dot(nn, d) > 0.0f) nn = nn * -1.0f;
+                    hit = true;
+                    t = th;
+                    normal = nn;
+                    hitp = o + d * th;
+                    mat = __float_as_int(T0[c1 ? 3 : 7].y);
+                }
+                st = (bi > -1 && steps < n_nodes) ? ST_TRAV : ST_SHADE;
+            }
+        } else {
+            // ---------------- TRAV: walk until a leaf is hit / the chain ends; yield to the
+            // other phases once enough lanes wait there
+            for (;;) {
+                if (st == ST_TRAV) {
+                    float4 lo = S.nodes[2 * bi], hi = S.nodes[2 * bi + 1];
+                    int a = __float_as_int(lo.w), b = __float_as_int(hi.w);
+                    bool hb = fast ? slab_fast(lo, hi, o, d, rd, t) : slab(lo, hi, o, d, t);
+                    if (COUNT) { c.nodes++; diag_tick(c.tw, c.tl); }
+                    steps++;
+                    bi = (hb && a >= 0) ? a : b;
+                    if (hb && a < 0) {
+                        leaf = ~a;
+                        st = ST_LEAF;
+                    } else if (bi < 0 || steps >= n_nodes) {
+                        st = ST_SHADE;
+                    }
+                }
+                unsigned long long mt = __ballot(st == ST_TRAV);
+                if (!mt) break;
+                if (__popcll(__ballot(st == ST_LEAF)) >= p.leaf_thresh) break;
+                if (__popcll(__ballot(st == ST_SHADE)) >= p.shade_thresh) break;
+            }
+        }
+    }
+    flush_counters<COUNT>(p, c);
+}
+
 // ACES film tonemap epilogue (screenQuadFrag.c:12-26) -> RGBA8, alpha 255.
 __global__ __launch_bounds__(256) void k_aces(const float4* __restrict__ src, uchar4* __restrict__ dst,
                                               long long n) {
@@ -683,11 +957,12 @@ struct pt_ctx {
     int n_nodes = 0, n_spheres = 0, n_mats = 0, n_slots = 0, scene_fast = 0;
     size_t lds_bytes = 0;
     unsigned persist_blocks = 2048;
+    int leaf_thresh = 24, shade_thresh = 40;
     bool scene_ok = false, cam_ok = false, counting = false;
     float cam[12] = {0};
     int variant = 0;
     float last_ms = 0.0f;
-    unsigned long long last_counts[5] = {0, 0, 0, 0, 0};
+    unsigned long long last_counts[16] = {0};
     bool count_pending = false;
     std::string err;
 };
@@ -735,7 +1010,7 @@ int pt_create(const pt_config* cfg, pt_ctx** out) {
     HIPCHK(c, hipMalloc(&c->accum, std::max<size_t>(px, 1) * sizeof(float4)));
     HIPCHK(c, hipMemset(c->accum, 0, std::max<size_t>(px, 1) * sizeof(float4)));
     HIPCHK(c, hipMalloc(&c->rgba8, std::max<size_t>(px, 1) * sizeof(uchar4)));
-    HIPCHK(c, hipMalloc(&c->d_counters, 8 * sizeof(unsigned long long)));
+    HIPCHK(c, hipMalloc(&c->d_counters, 16 * sizeof(unsigned long long)));
     HIPCHK(c, hipMalloc(&c->d_work, 64));
     int n_cu = 0;
     HIPCHK(c, hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, cfg->device));
@@ -916,8 +1191,18 @@ int pt_set_counting(pt_ctx* c, int enable) {
 
 int pt_set_kernel(pt_ctx* c, int variant) {
     if (!c) return PT_E_ARG;
-    if (variant < 0 || variant > 2) return fail(c, PT_E_ARG, "unknown kernel variant (0 wave+LDS, 1 tiled, 2 wave/global)");
+    if (variant < 0 || variant > 7)
+        return fail(c, PT_E_ARG, "unknown kernel variant (0 wave+LDS, 1 tiled, 2 wave/global, 3-5 occupancy probes, 6 state machine+LDS, 7 state machine/global)");
     c->variant = variant;
+    return PT_OK;
+}
+
+int pt_set_tuning(pt_ctx* c, int key, int value) {
+    if (!c) return PT_E_ARG;
+    if (value < 1 || value > 64) return fail(c, PT_E_ARG, "threshold must be in 1..64");
+    if (key == 0) c->leaf_thresh = value;
+    else if (key == 1) c->shade_thresh = value;
+    else return fail(c, PT_E_ARG, "unknown tuning key");
     return PT_OK;
 }
 
@@ -955,9 +1240,11 @@ int pt_render_async(pt_ctx* c, int frame_first, int n_frames, int acc_first) {
     p.n_slots = c->n_slots;
     p.n_mats = c->n_mats;
     p.scene_fast = c->scene_fast;
-    if (c->counting) HIPCHK(c, hipMemsetAsync(c->d_counters, 0, 8 * sizeof(unsigned long long), c->stream));
+    p.leaf_thresh = c->leaf_thresh;
+    p.shade_thresh = c->shade_thresh;
+    if (c->counting) HIPCHK(c, hipMemsetAsync(c->d_counters, 0, 16 * sizeof(unsigned long long), c->stream));
     if (c->rows_local == 0) return PT_OK;
-    bool use_lds = c->variant == 0 && c->lds_bytes <= kLdsSceneMax;
+    bool use_lds = (c->variant == 0 || (c->variant >= 3 && c->variant != 7)) && c->lds_bytes <= kLdsSceneMax;
     if (c->variant != 1) HIPCHK(c, hipMemsetAsync(c->d_work, 0, sizeof(unsigned), c->stream));
     hipEvent_t ev[2];
     for (int i = 0; i < 2; i++) {
@@ -983,12 +1270,24 @@ int pt_render_async(pt_ctx* c, int frame_first, int n_frames, int acc_first) {
         unsigned tiles = (unsigned)(((p.W + 7) / 8) * ((c->rows_local + 7) / 8));
         unsigned blocks = std::min<unsigned>(c->persist_blocks, std::max(1u, (tiles + 3) / 4));
         dim3 grid(blocks);
-        if (use_lds) {
-            if (c->counting) hipLaunchKernelGGL((k_render_wave<true, true>), grid, dim3(256), lds, c->stream, p);
-            else hipLaunchKernelGGL((k_render_wave<false, true>), grid, dim3(256), lds, c->stream, p);
+        if (c->variant >= 6) {
+            if (use_lds) {
+                if (c->counting) hipLaunchKernelGGL((k_render_sm<true, true>), grid, dim3(256), lds, c->stream, p);
+                else hipLaunchKernelGGL((k_render_sm<false, true>), grid, dim3(256), lds, c->stream, p);
+            } else {
+                if (c->counting) hipLaunchKernelGGL((k_render_sm<true, false>), grid, dim3(256), 0, c->stream, p);
+                else hipLaunchKernelGGL((k_render_sm<false, false>), grid, dim3(256), 0, c->stream, p);
+            }
+        } else if (use_lds) {
+            int mw = c->variant == 3 ? 5 : c->variant == 4 ? 6 : c->variant == 5 ? 8 : 1;
+#define PT_LAUNCH_W(MW)                                                                                        \
+    if (c->counting) hipLaunchKernelGGL((k_render_wave<true, true, MW>), grid, dim3(256), lds, c->stream, p);  \
+    else hipLaunchKernelGGL((k_render_wave<false, true, MW>), grid, dim3(256), lds, c->stream, p);
+            if (mw == 5) { PT_LAUNCH_W(5) } else if (mw == 6) { PT_LAUNCH_W(6) } else if (mw == 8) { PT_LAUNCH_W(8) } else { PT_LAUNCH_W(1) }
+#undef PT_LAUNCH_W
         } else {
-            if (c->counting) hipLaunchKernelGGL((k_render_wave<true, false>), grid, dim3(256), 0, c->stream, p);
-            else hipLaunchKernelGGL((k_render_wave<false, false>), grid, dim3(256), 0, c->stream, p);
+            if (c->counting) hipLaunchKernelGGL((k_render_wave<true, false, 1>), grid, dim3(256), 0, c->stream, p);
+            else hipLaunchKernelGGL((k_render_wave<false, false, 1>), grid, dim3(256), 0, c->stream, p);
         }
     }
     HIPCHK(c, hipGetLastError());
@@ -1011,7 +1310,7 @@ int pt_sync(pt_ctx* c) {
     }
     c->ev_pending.clear();
     if (c->count_pending) {
-        HIPCHK(c, hipMemcpy(c->last_counts, c->d_counters, 5 * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+        HIPCHK(c, hipMemcpy(c->last_counts, c->d_counters, 16 * sizeof(unsigned long long), hipMemcpyDeviceToHost));
         c->count_pending = false;
     }
     return PT_OK;
@@ -1090,10 +1389,16 @@ int pt_stream(pt_ctx* c, void** s) {
     return PT_OK;
 }
 
+int pt_stats_ex(pt_ctx* c, unsigned long long out[16]) {
+    if (!c || !out) return PT_E_ARG;
+    std::memcpy(out, c->last_counts, sizeof(c->last_counts));
+    return PT_OK;
+}
+
 int pt_stats(pt_ctx* c, double* ms, unsigned long long out[5]) {
     if (!c) return PT_E_ARG;
     if (ms) *ms = c->last_ms;
-    if (out) std::memcpy(out, c->last_counts, sizeof(c->last_counts));
+    if (out) std::memcpy(out, c->last_counts, 5 * sizeof(unsigned long long));
     return PT_OK;
 }
 

@@ -94,6 +94,8 @@ def lib():
             "pt_set_kernel": (ip, [vp, ip]),
             "pt_copy_rows_device": (ip, [vp, vp, C.c_size_t]),
             "pt_timing": (ip, [vp, C.POINTER(C.c_double), C.POINTER(ip), ip]),
+            "pt_stats_ex": (ip, [vp, np.ctypeslib.ndpointer(np.uint64)]),
+            "pt_set_tuning": (ip, [vp, ip, ip]),
         }
         for name, (res, args) in sig.items():
             fn = getattr(L, name)
@@ -257,6 +259,12 @@ class PathTracer:
     def set_kernel(self, variant):
         self._check(lib().pt_set_kernel(self.h, int(variant)))
 
+    def set_tuning(self, leaf_thresh=None, shade_thresh=None):
+        if leaf_thresh is not None:
+            self._check(lib().pt_set_tuning(self.h, 0, int(leaf_thresh)))
+        if shade_thresh is not None:
+            self._check(lib().pt_set_tuning(self.h, 1, int(shade_thresh)))
+
     def dispatch(self, frame, accumulate):
         """One glDispatchCompute with uniforms frame/accumulate (ogl_path_trace.h:176-183)."""
         self._check(lib().pt_render(self.h, frame, 1, accumulate))
@@ -288,6 +296,14 @@ class PathTracer:
         p, n = C.c_void_p(), C.c_size_t()
         self._check(lib().pt_accum_device(self.h, C.byref(p), C.byref(n)))
         return p.value, n.value
+
+    def diag(self):
+        """Lane utilisation per kernel phase from the last counting render."""
+        v = np.zeros(16, np.uint64)
+        self._check(lib().pt_stats_ex(self.h, v))
+        util = lambda w, l: float(v[l]) / max(1.0, 64.0 * float(v[w]))
+        return dict(trav_iters=int(v[5]), trav_util=util(5, 6), leaf_iters=int(v[7]), leaf_util=util(7, 8),
+                    seg_iters=int(v[9]), seg_util=util(9, 10))
 
     def copy_rows_device(self, dst_ptr, nbytes):
         self._check(lib().pt_copy_rows_device(self.h, C.c_void_p(dst_ptr), nbytes))

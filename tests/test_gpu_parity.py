@@ -11,7 +11,7 @@ import pt_host as H
 
 pytestmark = pytest.mark.gpu
 
-VARIANTS = [0, 1, 2]   # 0 persistent wave + LDS scene (default), 1 tiled, 2 persistent, global scene
+VARIANTS = [0, 1, 2, 6, 7]   # 0 wave+LDS (default), 1 tiled, 2 wave/global, 6 state machine+LDS, 7 state machine/global
 
 
 @pytest.fixture(params=VARIANTS, ids=lambda v: "v%d" % v)

@@ -25,24 +25,37 @@ def main():
     ap.add_argument("--width", type=int, default=1920)
     ap.add_argument("--height", type=int, default=1080)
     ap.add_argument("--bounces", type=int, default=8)
+    ap.add_argument("--tunings", default="24:40", help="leaf:shade thresholds for variants 6/7, comma list")
     a = ap.parse_args()
     sb = pt_host.setupBuffers(*pt_scenes.write_scene(a.scene, os.path.join(REPO, "scenes")))
     pt = pt_host.PathTracer(a.width, a.height, max_bounce=a.bounces)
     pt.upload(sb)
     seg = {}
-    configs = [(int(v), int(c)) for v in a.variants.split(",") for c in a.chunks.split(",")]
-    for v, c in configs:
+    configs = [(int(v), int(c), tu) for v in a.variants.split(",") for c in a.chunks.split(",")
+               for tu in (a.tunings.split(",") if int(v) >= 6 else ["-"])]
+    def apply(v, tu):
         pt.set_kernel(v)
+        if tu != "-":
+            lt, stt = tu.split(":")
+            pt.set_tuning(int(lt), int(stt))
+
+    for v, c, tu in configs:
+        apply(v, tu)
         pt.set_counting(True)
         total = 0
         for f0 in range(1, a.spp + 1, c):
             pt.render(f0, min(c, a.spp - f0 + 1), 0 if f0 == 1 else 1)
-            total += pt.stats()[1]["segments"]
+            st = pt.stats()[1]
+            total += st["segments"]
         pt.set_counting(False)
-        seg[(v, c)] = total
+        seg[(v, c, tu)] = total
+        dg = pt.diag()
+        print("variant %d chunk %d tune %s (last launch): %s  nodes/seg %.2f tri/seg %.2f" % (
+            v, c, tu, {k: (round(x, 3) if isinstance(x, float) else x) for k, x in dg.items()},
+            st["node_visits"] / st["segments"], st["tri_tests"] / st["segments"]), flush=True)
     for rnd in range(a.rounds):
-        for v, c in configs:
-            pt.set_kernel(v)
+        for v, c, tu in configs:
+            apply(v, tu)
             pt.timing(reset=True)
             t0 = time.perf_counter()
             for f0 in range(1, a.spp + 1, c):
@@ -50,8 +63,8 @@ def main():
             pt.sync()
             dt = time.perf_counter() - t0
             kms, n = pt.timing(reset=True)
-            print("round %d variant %d chunk %4d: %8.1f Mrays/s  wall %.1f ms  kernel %.1f ms (%d launches)  %.3f ms/frame"
-                  % (rnd, v, c, seg[(v, c)] / dt / 1e6, dt * 1e3, kms, n, dt * 1e3 / a.spp), flush=True)
+            print("round %d variant %d chunk %4d tune %-6s: %8.1f Mrays/s  wall %.1f ms  kernel %.1f ms (%d launches)  %.3f ms/frame"
+                  % (rnd, v, c, tu, seg[(v, c, tu)] / dt / 1e6, dt * 1e3, kms, n, dt * 1e3 / a.spp), flush=True)
     pt.close()
 
 
