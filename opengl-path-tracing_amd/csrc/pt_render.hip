@@ -414,6 +414,25 @@ __device__ __forceinline__ float tri_hit_bf(const float4* T, f3 o, f3 d, float t
     return ok ? t : -1.0f;
 }
 
+// Same test, but the plane distance is computed first and the edge tests run only if some
+// lane of the wave still needs them (a wave-uniform skip; per lane the verdict is the
+// same select as tri_hit_bf, so the bits are identical).
+__device__ __forceinline__ float tri_hit_lazy(const float4* T, f3 o, f3 d, float tbest, f3& n) {
+    float4 q0 = T[0], q1 = T[1], q2 = T[2], q3 = T[3];
+    n = mk(q0.w, q1.w, q2.w);
+    float t = -(pt::dot(n, o) + q3.x) / pt::dot(n, d);
+    bool ok = !(t < 0.0f) && (t < tbest);
+    if (__any(ok)) {
+        f3 v0 = mk(q0.x, q0.y, q0.z), v1 = mk(q1.x, q1.y, q1.z), v2 = mk(q2.x, q2.y, q2.z);
+        f3 p = o + d * t;
+        float e0 = pt::dot(n, pt::cross(v1 - v0, p - v0));
+        float e1 = pt::dot(n, pt::cross(v2 - v1, p - v1));
+        float e2 = pt::dot(n, pt::cross(v0 - v2, p - v2));
+        ok = ok && (e0 > 0.0f) && (e1 > 0.0f) && (e2 > 0.0f);
+    }
+    return ok ? t : -1.0f;
+}
+
 // calculateRayCollision with "while-while" scheduling of the stackless walk: each lane
 // advances through the link chain until it reaches a leaf whose box it hits (or the walk
 // ends), and only then do the lanes that stopped at leaves run the two triangle tests
@@ -671,8 +690,8 @@ __global__ __launch_bounds__(256, MINW) void k_render_wave(KParams p) {
 // =====================================================================================
 enum : int { ST_DONE = 0, ST_TRAV = 1, ST_LEAF = 2, ST_SHADE = 3 };
 
-template <bool COUNT, bool LDS>
-__global__ __launch_bounds__(256) void k_render_sm(KParams p) {
+template <bool COUNT, bool LDS, int MINW>
+__global__ __launch_bounds__(256, MINW) void k_render_sm(KParams p) {
     extern __shared__ float4 lds[];
     SceneView S;
     if (LDS) {
@@ -874,8 +893,8 @@ __global__ __launch_bounds__(256) void k_render_sm(KParams p) {
                 if (COUNT) { c.tri += 2; diag_tick(c.lw, c.ll); }
                 const float4* T0 = S.tris + 8 * (leaf >> 1);
                 f3 n0, n1;
-                float h1 = tri_hit_bf(T0, o, d, t, n0);
-                float h2 = tri_hit_bf(T0 + 4, o, d, t, n1);
+                float h1 = tri_hit_lazy(T0, o, d, t, n0);
+                float h2 = tri_hit_lazy(T0 + 4, o, d, t, n1);
                 bool c1 = h1 > 0.0001f && h1 < t && (h1 < h2 || h2 < 0.0001f);
                 bool c2 = !c1 && h2 > 0.0001f && h2 < t;
                 if (c1 || c2) {
@@ -957,7 +976,7 @@ struct pt_ctx {
     int n_nodes = 0, n_spheres = 0, n_mats = 0, n_slots = 0, scene_fast = 0;
     size_t lds_bytes = 0;
     unsigned persist_blocks = 2048;
-    int leaf_thresh = 24, shade_thresh = 40;
+    int leaf_thresh = 32, shade_thresh = 48;   // measured best on C2 (tools/probe.py sweep)
     bool scene_ok = false, cam_ok = false, counting = false;
     float cam[12] = {0};
     int variant = 0;
@@ -1191,8 +1210,8 @@ int pt_set_counting(pt_ctx* c, int enable) {
 
 int pt_set_kernel(pt_ctx* c, int variant) {
     if (!c) return PT_E_ARG;
-    if (variant < 0 || variant > 7)
-        return fail(c, PT_E_ARG, "unknown kernel variant (0 wave+LDS, 1 tiled, 2 wave/global, 3-5 occupancy probes, 6 state machine+LDS, 7 state machine/global)");
+    if (variant < 0 || variant > 3)
+        return fail(c, PT_E_ARG, "unknown kernel variant (0 state machine, 1 tiled, 2 while-while, 3 state machine / global scene)");
     c->variant = variant;
     return PT_OK;
 }
@@ -1244,7 +1263,9 @@ int pt_render_async(pt_ctx* c, int frame_first, int n_frames, int acc_first) {
     p.shade_thresh = c->shade_thresh;
     if (c->counting) HIPCHK(c, hipMemsetAsync(c->d_counters, 0, 16 * sizeof(unsigned long long), c->stream));
     if (c->rows_local == 0) return PT_OK;
-    bool use_lds = (c->variant == 0 || (c->variant >= 3 && c->variant != 7)) && c->lds_bytes <= kLdsSceneMax;
+    // variants: 0 state-machine persistent (default), 1 one-lane-per-pixel tiles,
+    // 2 while-while persistent, 3 = 0 with the scene forced to stay in global memory
+    bool use_lds = (c->variant == 0 || c->variant == 2) && c->lds_bytes <= kLdsSceneMax;
     if (c->variant != 1) HIPCHK(c, hipMemsetAsync(c->d_work, 0, sizeof(unsigned), c->stream));
     hipEvent_t ev[2];
     for (int i = 0; i < 2; i++) {
@@ -1270,25 +1291,17 @@ int pt_render_async(pt_ctx* c, int frame_first, int n_frames, int acc_first) {
         unsigned tiles = (unsigned)(((p.W + 7) / 8) * ((c->rows_local + 7) / 8));
         unsigned blocks = std::min<unsigned>(c->persist_blocks, std::max(1u, (tiles + 3) / 4));
         dim3 grid(blocks);
-        if (c->variant >= 6) {
-            if (use_lds) {
-                if (c->counting) hipLaunchKernelGGL((k_render_sm<true, true>), grid, dim3(256), lds, c->stream, p);
-                else hipLaunchKernelGGL((k_render_sm<false, true>), grid, dim3(256), lds, c->stream, p);
-            } else {
-                if (c->counting) hipLaunchKernelGGL((k_render_sm<true, false>), grid, dim3(256), 0, c->stream, p);
-                else hipLaunchKernelGGL((k_render_sm<false, false>), grid, dim3(256), 0, c->stream, p);
-            }
-        } else if (use_lds) {
-            int mw = c->variant == 3 ? 5 : c->variant == 4 ? 6 : c->variant == 5 ? 8 : 1;
-#define PT_LAUNCH_W(MW)                                                                                        \
-    if (c->counting) hipLaunchKernelGGL((k_render_wave<true, true, MW>), grid, dim3(256), lds, c->stream, p);  \
-    else hipLaunchKernelGGL((k_render_wave<false, true, MW>), grid, dim3(256), lds, c->stream, p);
-            if (mw == 5) { PT_LAUNCH_W(5) } else if (mw == 6) { PT_LAUNCH_W(6) } else if (mw == 8) { PT_LAUNCH_W(8) } else { PT_LAUNCH_W(1) }
-#undef PT_LAUNCH_W
+#define PT_LAUNCH(K, L, MW)                                                                                   \
+    if (c->counting) hipLaunchKernelGGL((K<true, L, MW>), grid, dim3(256), L ? lds : 0, c->stream, p);        \
+    else hipLaunchKernelGGL((K<false, L, MW>), grid, dim3(256), L ? lds : 0, c->stream, p);
+        if (c->variant == 0 || c->variant == 3) {
+            if (use_lds) { PT_LAUNCH(k_render_sm, true, 5) }
+            else { PT_LAUNCH(k_render_sm, false, 5) }
         } else {
-            if (c->counting) hipLaunchKernelGGL((k_render_wave<true, false, 1>), grid, dim3(256), 0, c->stream, p);
-            else hipLaunchKernelGGL((k_render_wave<false, false, 1>), grid, dim3(256), 0, c->stream, p);
+            if (use_lds) { PT_LAUNCH(k_render_wave, true, 1) }
+            else { PT_LAUNCH(k_render_wave, false, 1) }
         }
+#undef PT_LAUNCH
     }
     HIPCHK(c, hipGetLastError());
     HIPCHK(c, hipEventRecord(ev[1], c->stream));

@@ -11,7 +11,7 @@ import pt_host as H
 
 pytestmark = pytest.mark.gpu
 
-VARIANTS = [0, 1, 2, 6, 7]   # 0 wave+LDS (default), 1 tiled, 2 wave/global, 6 state machine+LDS, 7 state machine/global
+VARIANTS = [0, 1, 2, 3]   # 0 state machine (default), 1 tiled, 2 while-while, 3 state machine / global scene
 
 
 @pytest.fixture(params=VARIANTS, ids=lambda v: "v%d" % v)

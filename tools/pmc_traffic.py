@@ -1,0 +1,69 @@
+"""Reduce rocprofv3 PMC passes (tools/gpu_pmc.sh output) for the render kernel.
+
+Writes profiles/<tag>_pmc.json and profiles/traffic_latest.json:
+  hbm_bytes_per_launch = 2 * FETCH_SIZE * 1024 + WRITE_SIZE * 1024, per render launch.
+The factor 2 on FETCH_SIZE is the gfx950 correction of MI355X_MICROARCH.md §HBM (FETCH_SIZE
+reports half the bytes of wide 16-B/lane reads; the accumulator reads are float4 per lane);
+WRITE_SIZE is exact for 16-B/lane stores.  Raw values are kept alongside.
+"""
+import collections
+import csv
+import json
+import os
+import sys
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def load(d):
+    path = os.path.join(d, "run_counter_collection.csv")
+    agg = collections.defaultdict(lambda: collections.defaultdict(float))
+    dur = {}
+    for r in csv.DictReader(open(path)):
+        if "k_render" not in r["Kernel_Name"]:
+            continue
+        key = int(r["Dispatch_Id"])
+        agg[key][r["Counter_Name"]] += float(r["Counter_Value"])
+        dur[key] = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) * 1e-6
+    return agg, dur
+
+
+def main():
+    pmc = sys.argv[1] if len(sys.argv) > 1 else os.path.join(REPO, "gpurun_out", "pmc")
+    tag = sys.argv[2] if len(sys.argv) > 2 else "latest"
+    meta = dict(scene="cornell", width=1920, height=1080, chunk=64)
+    for a in sys.argv[3:]:
+        k, v = a.split("=")
+        meta[k] = int(v) if v.isdigit() else v
+    out = dict(meta)
+    per = collections.defaultdict(list)
+    for name in sorted(os.listdir(pmc)):
+        d = os.path.join(pmc, name)
+        if not os.path.isdir(d) or not os.path.exists(os.path.join(d, "run_counter_collection.csv")):
+            continue
+        agg, dur = load(d)
+        keys = sorted(agg)[1:] or sorted(agg)          # drop the warm-up launch when possible
+        for k in keys:
+            for cn, v in agg[k].items():
+                per[cn].append(v)
+            per["launch_ms_" + name].append(dur[k])
+    avg = {k: sum(v) / len(v) for k, v in per.items()}
+    out["counters_per_launch"] = avg
+    if "FETCH_SIZE" in avg and "WRITE_SIZE" in avg:
+        out["fetch_bytes_raw"] = avg["FETCH_SIZE"] * 1024
+        out["write_bytes"] = avg["WRITE_SIZE"] * 1024
+        out["hbm_bytes_per_launch"] = 2 * avg["FETCH_SIZE"] * 1024 + avg["WRITE_SIZE"] * 1024
+    if "SQ_THREAD_CYCLES_VALU" in avg:
+        out["valu_active_lanes_per_instr"] = avg["SQ_THREAD_CYCLES_VALU"] / max(avg["SQ_ACTIVE_INST_VALU"], 1)
+    if "SQ_WAVE_CYCLES" in avg and "SQ_WAIT_ANY" in avg:
+        tot = avg["SQ_WAVE_CYCLES"]
+        out["wave_cycle_split"] = {k: avg[k] / tot for k in ("SQ_ACTIVE_INST_ANY", "SQ_WAIT_INST_ANY", "SQ_WAIT_ANY") if k in avg}
+    os.makedirs(os.path.join(REPO, "profiles"), exist_ok=True)
+    for fn in ("%s_pmc.json" % tag, "traffic_latest.json"):
+        with open(os.path.join(REPO, "profiles", fn), "w") as fh:
+            json.dump(out, fh, indent=1, sort_keys=True)
+    print(json.dumps({k: v for k, v in out.items() if k != "counters_per_launch"}, indent=1))
+
+
+if __name__ == "__main__":
+    main()
