@@ -690,7 +690,7 @@ __global__ __launch_bounds__(256, MINW) void k_render_wave(KParams p) {
 // =====================================================================================
 enum : int { ST_DONE = 0, ST_TRAV = 1, ST_LEAF = 2, ST_SHADE = 3 };
 
-template <bool COUNT, bool LDS, int MINW>
+template <bool COUNT, bool LDS, int MINW, bool MULTI>
 __global__ __launch_bounds__(256, MINW) void k_render_sm(KParams p) {
     extern __shared__ float4 lds[];
     SceneView S;
@@ -724,14 +724,15 @@ __global__ __launch_bounds__(256, MINW) void k_render_sm(KParams p) {
     bool fresh = true;        // SHADE without a finished segment (start / after fetch)
     bool need_ray = true;     // next SHADE must start a new camera ray
     int lx = -1, y = 0;
-    size_t aidx = 0;
+    int aidx = 0;             // rows_local * W < 2^31 (checked at pt_create)
     int k = 0, r = 0, bounce = 0;
     float4 acc = make_float4(0, 0, 0, 0);
     f3 psum = mk(0, 0, 0), o = mk(0, 0, 0), d = mk(0, 0, 1), inc = mk(0, 0, 0), col = mk(1, 1, 1);
     uint32_t state = 0;
-    // segment state
+    // segment state (the hit point is recomputed at shading time as o + d*t: the same
+    // operation the reference performs when it accepts the hit, on the same final t)
     bool fast = false, hit = false;
-    f3 rd = mk(0, 0, 0), normal = mk(0, 0, 0), hitp = mk(0, 0, 0);
+    f3 rd = mk(0, 0, 0), normal = mk(0, 0, 0);
     float t = 0.0f;
     int mat = 0, bi = -1, leaf = 0, steps = 0;
 
@@ -747,6 +748,7 @@ __global__ __launch_bounds__(256, MINW) void k_render_sm(KParams p) {
                 bool finished = false;
                 f3 rgb = inc;
                 if (hit && pt::length(col) > 0.01f) {
+                    const f3 hitp = o + d * t;
                     if (p.mode == 2) {
                         rgb = (normal + mk(1, 1, 1)) * 0.5f;
                         finished = true;
@@ -790,13 +792,19 @@ __global__ __launch_bounds__(256, MINW) void k_render_sm(KParams p) {
                 }
                 need_ray = finished;
                 if (finished) {
-                    psum = psum + rgb;
-                    r++;
-                    if (r >= p.rpp) {
+                    if (MULTI) {          // raysPerPixel > 1: pixel = 0 + sum of rays, / rpp
+                        psum = psum + rgb;
+                        r++;
+                        if (r >= p.rpp) {
+                            int f = p.frame_first + k;
+                            acc = accumulate(acc, psum / (float)p.rpp, f, k > 0 || p.acc_first == 1);
+                            psum = mk(0, 0, 0);
+                            r = 0;
+                            k++;
+                        }
+                    } else {              // raysPerPixel == 1: pixel = (0 + rgb) / 1
                         int f = p.frame_first + k;
-                        acc = accumulate(acc, psum / (float)p.rpp, f, k > 0 || p.acc_first == 1);
-                        psum = mk(0, 0, 0);
-                        r = 0;
+                        acc = accumulate(acc, (mk(0, 0, 0) + rgb) / 1.0f, f, k > 0 || p.acc_first == 1);
                         k++;
                     }
                 }
@@ -826,7 +834,7 @@ __global__ __launch_bounds__(256, MINW) void k_render_sm(KParams p) {
                         if (cx < p.W && crow < p.rows_local && cx < p.x_limit && cy < p.y_limit) {
                             lx = cx;
                             y = cy;
-                            aidx = (size_t)crow * p.W + cx;
+                            aidx = crow * p.W + cx;
                             k = 0;
                             r = 0;
                             psum = mk(0, 0, 0);
@@ -877,7 +885,6 @@ __global__ __launch_bounds__(256, MINW) void k_render_sm(KParams p) {
                             hit = true;
                             t = ht;
                             normal = pn;
-                            hitp = o + d * ht;
                             mat = __float_as_int(S.spheres[2 * si + 1].x);
                         }
                     }
@@ -904,7 +911,6 @@ __global__ __launch_bounds__(256, MINW) void k_render_sm(KParams p) {
                     hit = true;
                     t = th;
                     normal = nn;
-                    hitp = o + d * th;
                     mat = __float_as_int(T0[c1 ? 3 : 7].y);
                 }
                 st = (bi > -1 && steps < n_nodes) ? ST_TRAV : ST_SHADE;
@@ -1024,6 +1030,7 @@ int pt_create(const pt_config* cfg, pt_ctx** out) {
     HIPCHK(c, hipSetDevice(cfg->device));
     int rank = c->cfg.rank, world = c->cfg.world;
     c->rows_local = cfg->height > rank ? (cfg->height - rank + world - 1) / world : 0;
+    if ((long long)c->rows_local * cfg->width >= (1LL << 31)) return fail(c, PT_E_ARG, "framebuffer exceeds 2^31 pixels");
     size_t px = (size_t)c->rows_local * cfg->width;
     HIPCHK(c, hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
     HIPCHK(c, hipMalloc(&c->accum, std::max<size_t>(px, 1) * sizeof(float4)));
@@ -1294,9 +1301,16 @@ int pt_render_async(pt_ctx* c, int frame_first, int n_frames, int acc_first) {
 #define PT_LAUNCH(K, L, MW)                                                                                   \
     if (c->counting) hipLaunchKernelGGL((K<true, L, MW>), grid, dim3(256), L ? lds : 0, c->stream, p);        \
     else hipLaunchKernelGGL((K<false, L, MW>), grid, dim3(256), L ? lds : 0, c->stream, p);
+#define PT_LAUNCH_SM(L, M)                                                                                    \
+    if (c->counting) hipLaunchKernelGGL((k_render_sm<true, L, 5, M>), grid, dim3(256), L ? lds : 0, c->stream, p); \
+    else hipLaunchKernelGGL((k_render_sm<false, L, 5, M>), grid, dim3(256), L ? lds : 0, c->stream, p);
         if (c->variant == 0 || c->variant == 3) {
-            if (use_lds) { PT_LAUNCH(k_render_sm, true, 5) }
-            else { PT_LAUNCH(k_render_sm, false, 5) }
+            bool multi = p.rpp > 1;
+            if (use_lds && multi) { PT_LAUNCH_SM(true, true) }
+            else if (use_lds) { PT_LAUNCH_SM(true, false) }
+            else if (multi) { PT_LAUNCH_SM(false, true) }
+            else { PT_LAUNCH_SM(false, false) }
+#undef PT_LAUNCH_SM
         } else {
             if (use_lds) { PT_LAUNCH(k_render_wave, true, 1) }
             else { PT_LAUNCH(k_render_wave, false, 1) }

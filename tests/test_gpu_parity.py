@@ -157,6 +157,18 @@ def test_exact_reciprocal_guard_fallback(cornell_scene, V):
     assert_bitwise(got, want, "scaled scene")
 
 
+def test_rays_per_pixel(cornell_scene, V):
+    """raysPerPixel > 1 (computeShader.c:507-544): rays share the RNG stream of the frame."""
+    want = O.render(cornell_scene, 32, 24, max_bounce=6, n_frames=2, rpp=3)
+    pt = H.PathTracer(32, 24, max_bounce=6, rays_per_pixel=3)
+    pt.set_kernel(V)
+    pt.upload(cornell_scene)
+    pt.render(1, 2, 0)
+    got = pt.read_rgba32f()
+    pt.close()
+    assert_bitwise(got, want, "rpp 3")
+
+
 def test_aces_epilogue(cornell_scene):
     pt = H.PathTracer(64, 64, max_bounce=5)
     pt.upload(cornell_scene)
