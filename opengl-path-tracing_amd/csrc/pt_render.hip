@@ -982,7 +982,9 @@ struct pt_ctx {
     int n_nodes = 0, n_spheres = 0, n_mats = 0, n_slots = 0, scene_fast = 0;
     size_t lds_bytes = 0;
     unsigned persist_blocks = 2048;
-    int leaf_thresh = 32, shade_thresh = 48;   // measured best on C2 (tools/probe.py sweep)
+    // 0 = automatic: 32/48 when the scene is staged in LDS (best on C2), 8/32 when the walk
+    // reads global memory (latency-bound; best on the C3/C4 stand-ins) -- tools/probe.py sweeps
+    int leaf_thresh = 0, shade_thresh = 0;
     bool scene_ok = false, cam_ok = false, counting = false;
     float cam[12] = {0};
     int variant = 0;
@@ -1225,7 +1227,7 @@ int pt_set_kernel(pt_ctx* c, int variant) {
 
 int pt_set_tuning(pt_ctx* c, int key, int value) {
     if (!c) return PT_E_ARG;
-    if (value < 1 || value > 64) return fail(c, PT_E_ARG, "threshold must be in 1..64");
+    if (value < 0 || value > 64) return fail(c, PT_E_ARG, "threshold must be in 1..64 (0 = automatic)");
     if (key == 0) c->leaf_thresh = value;
     else if (key == 1) c->shade_thresh = value;
     else return fail(c, PT_E_ARG, "unknown tuning key");
@@ -1266,8 +1268,11 @@ int pt_render_async(pt_ctx* c, int frame_first, int n_frames, int acc_first) {
     p.n_slots = c->n_slots;
     p.n_mats = c->n_mats;
     p.scene_fast = c->scene_fast;
-    p.leaf_thresh = c->leaf_thresh;
-    p.shade_thresh = c->shade_thresh;
+    {
+        bool lds_scene = c->lds_bytes <= kLdsSceneMax && c->variant != 3;
+        p.leaf_thresh = c->leaf_thresh ? c->leaf_thresh : (lds_scene ? 32 : 8);
+        p.shade_thresh = c->shade_thresh ? c->shade_thresh : (lds_scene ? 48 : 32);
+    }
     if (c->counting) HIPCHK(c, hipMemsetAsync(c->d_counters, 0, 16 * sizeof(unsigned long long), c->stream));
     if (c->rows_local == 0) return PT_OK;
     // variants: 0 state-machine persistent (default), 1 one-lane-per-pixel tiles,

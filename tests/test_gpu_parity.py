@@ -169,6 +169,22 @@ def test_rays_per_pixel(cornell_scene, V):
     assert_bitwise(got, want, "rpp 3")
 
 
+@pytest.fixture(scope="module", params=["bunny", "sponza"])
+def big_scene(request, tmp_path_factory):
+    import pt_scenes
+    d = str(tmp_path_factory.mktemp("scenes"))
+    return H.setupBuffers(*pt_scenes.write_scene(request.param, d))
+
+
+@pytest.mark.parametrize("variant", [0, 2])
+def test_large_scene_bitwise(big_scene, variant):
+    """C3/C4 stand-ins (69k / 249k triangles): the scene no longer fits the LDS staging
+    budget, so the kernels walk the BVH from global memory."""
+    want = O.render(big_scene, 48, 27, max_bounce=8, n_frames=2)
+    got = gpu_render(big_scene, 48, 27, max_bounce=8, n_frames=2, variant=variant)
+    assert_bitwise(got, want, "large scene")
+
+
 def test_aces_epilogue(cornell_scene):
     pt = H.PathTracer(64, 64, max_bounce=5)
     pt.upload(cornell_scene)

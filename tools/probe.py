@@ -32,7 +32,7 @@ def main():
     pt.upload(sb)
     seg = {}
     configs = [(int(v), int(c), tu) for v in a.variants.split(",") for c in a.chunks.split(",")
-               for tu in (a.tunings.split(",") if int(v) >= 6 else ["-"])]
+               for tu in (a.tunings.split(",") if int(v) in (0, 3) else ["-"])]
     def apply(v, tu):
         pt.set_kernel(v)
         if tu != "-":
