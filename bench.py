@@ -2,18 +2,19 @@
 """Benchmark of the MI355X path-tracing hot path (BASELINE.json metric:
 "Mrays/sec + ms/frame @1920x1080, 8 bounces, 1/2/4/8 MI355X").
 
-Workload (N=1 default = config C2): the Cornell box (36 tris + the
-reference's metal sphere), 1920x1080, 8 bounces (loop i <= 8), frames 1..1024 with
-accumulate=0 on frame 1.  One *step* = one full progressive render of `spp` frames, issued
-as ceil(spp/chunk) fused launches, plus (N>1) the RCCL all-gather that assembles the
-row-interleaved image.  Inputs (scene, accumulator) are resident in HBM before timing.
+Default workload = config C2: the Cornell box (36 tris + the reference's
+metal sphere), 1920x1080, 8 bounces (loop i <= 8), frames 1..1024 with accumulate=0 on
+frame 1.  One *step* = one full progressive render of `spp` frames, issued as
+ceil(spp/chunk) fused launches (C5: replays of a captured hipGraph), plus for N>1 the
+RCCL all-gather that assembles the row-interleaved frame.  Scene and accumulator are
+resident in HBM before timing starts.
 
-value = segments (ray-scene queries, computeShader.c:450) of all ranks / max-over-ranks
-wall time, in Mrays/s.  Segment counts come from an untimed counting pass of the same
-frames (reference traversal semantics, bit-identical image).
+value = ray segments (calculateRayCollision calls, computeShader.c:450) of all ranks /
+max-over-ranks wall time, in Mrays/s.  Segment counts come from an untimed counting pass
+over the same frames (reference traversal semantics; identical image).
 
-Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--spp S] [--chunk C]
-       (N>1: python -m torch.distributed.run --nproc-per-node N bench.py --gpus N ...)
+Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--config C2|C3|C4|C5]
+N>1:   python -m torch.distributed.run --nproc-per-node N bench.py --gpus N ...
 """
 from __future__ import annotations
 
@@ -28,13 +29,21 @@ PKG = os.path.join(REPO, "opengl-path-tracing_amd")
 sys.path.insert(0, PKG)
 
 METRIC = "Mrays/sec + ms/frame @1920×1080, 8 bounces, 1/2/4/8 MI355X"
-HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
+
+# scene, W, H, spp, bounces, frames per launch, graph launches/replay
+CONFIGS = {
+    "C2": ("cornell", 1920, 1080, 1024, 8, 64, 0),
+    "C3": ("bunny", 1920, 1080, 256, 8, 32, 0),
+    "C4": ("sponza", 1920, 1080, 256, 8, 32, 0),
+    "C5": ("cornell", 3840, 2160, 4096, 8, 64, 8),
+}
 
 
 def algorithmic_bytes(cnt, pixels, first_launch_plain):
     """40 B/node visit + 36 B/tri test + 16 B/sphere test + 52 B/hit,
     plus 32 B per pixel per launch for the accumulator read+write (16 B when the launch
-    starts with accumulate=0 and so only writes)."""
+    starts with accumulate=0 and only writes)."""
     b = 40 * cnt["node_visits"] + 36 * cnt["tri_tests"] + 16 * cnt["sphere_tests"] + 52 * cnt["hits"]
     return b + pixels * (16 if first_launch_plain else 32)
 
@@ -44,67 +53,90 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--spp", type=int, default=1024)
-    ap.add_argument("--chunk", type=int, default=64, help="frames fused per kernel launch")
-    ap.add_argument("--width", type=int, default=1920)
-    ap.add_argument("--height", type=int, default=1080)
-    ap.add_argument("--bounces", type=int, default=8)
-    ap.add_argument("--scene", default="cornell", choices=["cornell", "bunny", "sponza"])
+    ap.add_argument("--config", default="C2", choices=sorted(CONFIGS))
+    ap.add_argument("--spp", type=int, default=None)
+    ap.add_argument("--chunk", type=int, default=None, help="frames fused per kernel launch")
+    ap.add_argument("--width", type=int, default=None)
+    ap.add_argument("--height", type=int, default=None)
+    ap.add_argument("--bounces", type=int, default=None)
     ap.add_argument("--variant", type=int, default=0)
     ap.add_argument("--cpu-spp", type=int, default=1, help="spp of the bounded CPU-baseline sample")
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
+                    help="nccl = RCCL over xGMI (default); gloo = CPU rehearsal of the N>1 path")
     ap.add_argument("--traffic-json", default=os.path.join(REPO, "profiles", "traffic_latest.json"),
-                    help="PMC-derived HBM bytes per launch (written by tools/pmc_traffic.py)")
+                    help="PMC-derived HBM bytes per launch (tools/pmc_traffic.py)")
     args = ap.parse_args()
 
-    import numpy as np
     import torch
 
     import pt_host
     import pt_scenes
 
+    scene, W, H, spp, bounces, chunk, graph_launches = CONFIGS[args.config]
+    W = args.width or W
+    H = args.height or H
+    spp = args.spp or spp
+    bounces = args.bounces if args.bounces is not None else bounces
+    chunk = min(args.chunk or chunk, spp)
+
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     distributed = world > 1
+    ndev = max(1, torch.cuda.device_count())
+    device = local_rank % ndev
     if distributed:
         import torch.distributed as dist
         import pt_dist
-        torch.cuda.set_device(local_rank)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+        if args.dist_backend == "nccl":
+            torch.cuda.set_device(device)
+            dist.init_process_group("nccl", device_id=torch.device("cuda", device))
+        else:
+            dist.init_process_group("gloo")
 
     def barrier():
         if distributed:
             dist.barrier()
 
-    W, H, spp, chunk = args.width, args.height, args.spp, min(args.chunk, args.spp)
     scene_dir = os.path.join(REPO, "scenes")
-    obj, mtl = pt_scenes.write_scene(args.scene, scene_dir) if rank == 0 or not distributed else (None, None)
+    if rank == 0:
+        obj, mtl = pt_scenes.write_scene(scene, scene_dir)
     barrier()
-    if obj is None:
-        obj = os.path.join(scene_dir, "%sobj.txt" % args.scene)
-        mtl = os.path.join(scene_dir, "%smtl.txt" % args.scene)
+    obj = os.path.join(scene_dir, "%sobj.txt" % scene)
+    mtl = os.path.join(scene_dir, "%smtl.txt" % scene)
     sb = pt_host.setupBuffers(obj, mtl)
-    pt = pt_host.PathTracer(W, H, max_bounce=args.bounces, display_mode=1, device=local_rank,
-                            rank=rank, world=world)
+    pt = pt_host.PathTracer(W, H, max_bounce=bounces, display_mode=1, device=device, rank=rank, world=world)
     pt.set_kernel(args.variant)
     pt.upload(sb)
     launches = [(f0, min(chunk, spp - (f0 - 1))) for f0 in range(1, spp + 1, chunk)]
+    use_graph = graph_launches > 0 and spp % (chunk * graph_launches) == 0
+    if use_graph:
+        pt.progressive_setup(chunk, graph_launches)
+        replays = spp // (chunk * graph_launches)
 
     if distributed:
         rmax = pt_dist.rows_max(H, world)
-        send = torch.zeros((rmax, W, 4), dtype=torch.float32, device="cuda")
+        dev = "cuda" if args.dist_backend == "nccl" else "cpu"
+        send = torch.zeros((rmax, W, 4), dtype=torch.float32, device=dev)
 
     def step():
-        for f0, n in launches:
-            pt.render_async(f0, n, 0 if f0 == 1 else 1)
+        if use_graph:
+            pt.progressive_reset(1)
+            pt.progressive_run(replays, sync=False)
+        else:
+            for f0, n in launches:
+                pt.render_async(f0, n, 0 if f0 == 1 else 1)
         pt.sync()
         if distributed:
-            nbytes = pt.rows_local * W * 16
-            pt.copy_rows_device(send.data_ptr(), nbytes)
+            if args.dist_backend == "nccl":
+                pt.copy_rows_device(send.data_ptr(), pt.rows_local * W * 16)
+            else:
+                send[: pt.rows_local] = torch.from_numpy(pt.read_rgba32f())
             img = pt_dist.gather_image(send, H, world)
-            torch.cuda.synchronize()
+            if args.dist_backend == "nccl":
+                torch.cuda.synchronize()
             return img
         return None
 
@@ -120,8 +152,11 @@ def main():
     barrier()
     dt = time.perf_counter() - t0
     kern_ms, n_launch = pt.timing(reset=True)
+    if use_graph:
+        n_launch = args.steps * replays * graph_launches      # events bracket whole replays
+    coll_dev = "cuda" if args.dist_backend == "nccl" else "cpu"
     if distributed:
-        t = torch.tensor([dt], dtype=torch.float64, device="cuda")
+        t = torch.tensor([dt], dtype=torch.float64, device=coll_dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
 
@@ -137,11 +172,11 @@ def main():
         alg_bytes += algorithmic_bytes(cnt, pt.rows_local * W, f0 == 1)
     pt.set_counting(False)
     if distributed:
-        v = torch.tensor([tot["segments"], alg_bytes], dtype=torch.float64, device="cuda")
+        v = torch.tensor([tot["segments"], alg_bytes], dtype=torch.float64, device=coll_dev)
         dist.all_reduce(v, op=dist.ReduceOp.SUM)
-        seg_all, bytes_all = float(v[0]), float(v[1])
+        seg_all = float(v[0])
     else:
-        seg_all, bytes_all = float(tot["segments"]), float(alg_bytes)
+        seg_all = float(tot["segments"])
 
     ms_per_step = dt / args.steps * 1e3
     value = seg_all * args.steps / dt / 1e6
@@ -153,7 +188,8 @@ def main():
     try:
         with open(args.traffic_json) as fh:
             tj = json.load(fh)
-        if tj.get("width") == W and tj.get("height") == H and tj.get("chunk") == chunk and tj.get("scene") == args.scene:
+        if (tj.get("width"), tj.get("height"), tj.get("chunk"), tj.get("scene")) == (W, H, chunk, scene) \
+                and world == 1:
             traffic = tj.get("hbm_bytes_per_launch")
     except (OSError, ValueError):
         pass
@@ -164,34 +200,35 @@ def main():
         import oracle_lib
         threads = min(args.cpu_threads, os.cpu_count() or 1)
         t1 = time.perf_counter()
-        _, ccnt = oracle_lib.render(sb, W, H, max_bounce=args.bounces, n_frames=args.cpu_spp,
-                                    threads=threads, counters=True)
+        _, ccnt = oracle_lib.render(sb, W, H, max_bounce=bounces, n_frames=args.cpu_spp, threads=threads,
+                                    counters=True)
         cdt = time.perf_counter() - t1
-        cpu = {"value": round(float(ccnt[0]) / cdt / 1e6, 3), "unit": "Mrays/s", "cores": threads,
-               "kind": "port",
-               "sample": "CPU restatement of computeShader.c semantics (oracle/pt_oracle.cpp, -O3, "
-                         "%d threads), same scene/camera/bounces at %dx%d, frames 1..%d (%d segments, %.2f s); "
-                         "ms/frame extrapolated = %.1f" % (threads, W, H, args.cpu_spp, int(ccnt[0]), cdt,
-                                                            cdt * 1e3 / args.cpu_spp)}
+        cpu = {"value": round(float(ccnt[0]) / cdt / 1e6, 3), "unit": "Mrays/s", "cores": threads, "kind": "port",
+               "sample": "CPU restatement of computeShader.c semantics (oracle/pt_oracle.cpp, -O3, %d threads), "
+                         "same scene/camera/bounces at %dx%d, frames 1..%d (%d segments, %.2f s); "
+                         "ms/frame = %.1f" % (threads, W, H, args.cpu_spp, int(ccnt[0]), cdt, cdt * 1e3 / args.cpu_spp)}
 
     if rank == 0:
         line = {
             "metric": METRIC, "value": round(value, 3), "unit": "Mrays/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_per_step, 3),
-            "higher_is_better": True, "scaling": "strong",
-            "vs_baseline": None, "dtype": "f32", "data": "synthetic",
-            "config": {"workload": "C2: %s %dx%d, %d spp (frames 1..%d), %d bounces (i<=%d), AA+sky+sphere on"
-                       % (args.scene, W, H, spp, spp, args.bounces, args.bounces),
-                       "scene": args.scene, "width": W, "height": H, "spp": spp, "max_bounce": args.bounces,
+            "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "f32",
+            "data": "synthetic",
+            "config": {"workload": "%s: %s %dx%d, %d spp (frames 1..%d), %d bounces (i<=%d), AA+sky+sphere on%s"
+                       % (args.config, scene, W, H, spp, spp, bounces, bounces,
+                          ", hipGraph sample loop" if use_graph else ""),
+                       "scene": scene, "width": W, "height": H, "spp": spp, "max_bounce": bounces,
                        "frames_per_launch": chunk, "kernel_variant": args.variant,
-                       "parallelism": "row-interleaved image split x%d + RCCL all-gather" % world if world > 1
-                       else "single GPU"},
+                       "parallelism": ("row-interleaved image split x%d + %s all-gather"
+                                       % (world, "RCCL" if args.dist_backend == "nccl" else "gloo"))
+                       if world > 1 else "single GPU"},
             "ms_per_frame": round(ms_per_step / spp, 4),
             "segments_per_step": int(seg_all),
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-                         "basis": "algorithmic bytes (SURVEY.md §8(d)) per launch / avg launch time (HIP events, "
-                                  "%d launches); cache-resident scene so frac can exceed 1" % n_launch,
+                         "basis": "algorithmic bytes (SURVEY.md §8(d)) per launch / avg launch time (HIP events "
+                                  "on the render stream, %d launches); the scene is cache/LDS-resident so frac "
+                                  "can exceed 1; traffic = PMC HBM bytes per launch (profiles/)" % n_launch,
                          "avg_launch_ms": round(avg_launch_ms, 3)},
             "cpu_baseline": cpu,
         }

@@ -70,6 +70,17 @@ int pt_render(pt_ctx* ctx, int frame_first, int n_frames, int accumulate_first);
 int pt_render_async(pt_ctx* ctx, int frame_first, int n_frames, int accumulate_first);
 int pt_sync(pt_ctx* ctx);
 
+/* Progressive rendering as a replayed hipGraph (the reference's endless render loop,
+ * ogl_path_trace.h:160-204, without a host round trip per frame): setup captures
+ * `launches_per_replay` launches of `frames_per_launch` frames each plus a device-side
+ * frame-counter advance; every replay renders the next frames_per_launch*launches frames.
+ * Frame 1 is rendered with accumulate = 0 (a reset), later frames accumulate.  reset()
+ * sets the next frame number (1 = restart accumulation).  The graph is dropped whenever
+ * the scene, camera, kernel or tuning changes.  run() is asynchronous (pt_sync waits). */
+int pt_progressive_setup(pt_ctx* ctx, int frames_per_launch, int launches_per_replay);
+int pt_progressive_reset(pt_ctx* ctx, int next_frame);
+int pt_progressive_run(pt_ctx* ctx, int replays);
+
 /* Local rows owned by this context: rows y = rank + k*world, k < rows_local. */
 int pt_rows(const pt_ctx* ctx, int* rows_local, int* row0, int* row_stride);
 

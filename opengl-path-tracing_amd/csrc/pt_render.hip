@@ -51,7 +51,23 @@ struct KParams {
     int n_slots, n_mats;           // triangle slots / materials (LDS staging sizes)
     int scene_fast;                // every box coordinate inside the exact-reciprocal guard
     int leaf_thresh, shade_thresh; // wave scheduling thresholds of the state-machine kernel
+    const int* frame_dev;          // progressive graph: device frame counter (null = use frame_first)
+    int frame_offset;              // this launch's frame offset from *frame_dev
 };
+
+// Progressive mode (hipGraph replay): the frame range comes from a device counter, and
+// accumulate = 0 only on frame 1 -- the reference's run loop after a reset
+// (ogl_path_trace.h:164,199-203).
+__device__ __forceinline__ void resolve_frames(KParams& p) {
+    if (p.frame_dev) {
+        p.frame_first = *p.frame_dev + p.frame_offset;
+        p.acc_first = p.frame_first != 1;
+    }
+}
+
+__global__ void k_advance_frames(int* frame_dev, int n) {
+    if (threadIdx.x == 0 && blockIdx.x == 0) *frame_dev += n;
+}
 
 struct Cnt {
     uint32_t seg, nodes, tri, sph, hits;
@@ -265,6 +281,7 @@ __device__ __forceinline__ void flush_counters(const KParams& p, const Cnt& c) {
 // read + write per launch), 16x16-pixel workgroups of four 8x8 wave tiles.
 template <bool COUNT>
 __global__ __launch_bounds__(256) void k_render_tiled(KParams p) {
+    resolve_frames(p);
     int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     int lx = blockIdx.x * 16 + (wave & 1) * 8 + (lane & 7);
     int lrow = blockIdx.y * 16 + (wave >> 1) * 8 + (lane >> 3);
@@ -510,6 +527,7 @@ __device__ __forceinline__ bool collide_ww(const SceneView& S, int n_nodes, int 
 
 template <bool COUNT, bool LDS, int MINW>
 __global__ __launch_bounds__(256, MINW) void k_render_wave(KParams p) {
+    resolve_frames(p);
     extern __shared__ float4 lds[];
     SceneView S;
     if (LDS) {
@@ -692,6 +710,7 @@ enum : int { ST_DONE = 0, ST_TRAV = 1, ST_LEAF = 2, ST_SHADE = 3 };
 
 template <bool COUNT, bool LDS, int MINW, bool MULTI>
 __global__ __launch_bounds__(256, MINW) void k_render_sm(KParams p) {
+    resolve_frames(p);
     extern __shared__ float4 lds[];
     SceneView S;
     if (LDS) {
@@ -979,6 +998,10 @@ struct pt_ctx {
     float4 *d_nodes = nullptr, *d_tris = nullptr, *d_mats = nullptr, *d_spheres = nullptr;
     unsigned long long* d_counters = nullptr;
     unsigned int* d_work = nullptr;
+    int* d_frame = nullptr;                      // progressive graph frame counter
+    hipGraph_t graph = nullptr;
+    hipGraphExec_t graph_exec = nullptr;
+    int graph_frames = 0;
     int n_nodes = 0, n_spheres = 0, n_mats = 0, n_slots = 0, scene_fast = 0;
     size_t lds_bytes = 0;
     unsigned persist_blocks = 2048;
@@ -993,6 +1016,8 @@ struct pt_ctx {
     bool count_pending = false;
     std::string err;
 };
+
+static void drop_graph(pt_ctx* c);   // a captured graph bakes in scene/camera/config
 
 static int fail(pt_ctx* c, int code, const std::string& msg) {
     if (c) c->err = msg;
@@ -1052,8 +1077,10 @@ int pt_create(const pt_config* cfg, pt_ctx** out) {
 void pt_destroy(pt_ctx* c) {
     if (!c) return;
     if (c->stream) (void)hipStreamSynchronize(c->stream);
+    drop_graph(c);
     free_scene(c);
     (void)hipFree(c->accum); (void)hipFree(c->rgba8); (void)hipFree(c->d_counters); (void)hipFree(c->d_work);
+    (void)hipFree(c->d_frame);
     for (auto& pr : c->ev_pending) { c->ev_free.push_back(pr.first); c->ev_free.push_back(pr.second); }
     for (hipEvent_t e : c->ev_free) (void)hipEventDestroy(e);
     if (c->stream) (void)hipStreamDestroy(c->stream);
@@ -1168,6 +1195,7 @@ int pt_upload_scene(pt_ctx* c, const float* tris, int n_tris, const float* bvh, 
         ds[2 * (size_t)i] = make_float4(s[0], s[1], s[2], s[3] * s[3]);
         ds[2 * (size_t)i + 1] = make_float4(mb, 0, 0, 0);
     }
+    drop_graph(c);
     free_scene(c);
     HIPCHK(c, hipMalloc(&c->d_nodes, dn.size() * sizeof(float4)));
     HIPCHK(c, hipMalloc(&c->d_tris, dt.size() * sizeof(float4)));
@@ -1208,6 +1236,7 @@ int pt_set_camera(pt_ctx* c, const float cam[12]) {
     float v[12] = {pos.x, pos.y, pos.z, fwd.x, fwd.y, fwd.z, right.x, right.y, right.z, up.x, up.y, up.z};
     std::memcpy(c->cam, v, sizeof(v));
     c->cam_ok = true;
+    drop_graph(c);
     return PT_OK;
 }
 
@@ -1222,6 +1251,7 @@ int pt_set_kernel(pt_ctx* c, int variant) {
     if (variant < 0 || variant > 3)
         return fail(c, PT_E_ARG, "unknown kernel variant (0 state machine, 1 tiled, 2 while-while, 3 state machine / global scene)");
     c->variant = variant;
+    drop_graph(c);
     return PT_OK;
 }
 
@@ -1231,14 +1261,14 @@ int pt_set_tuning(pt_ctx* c, int key, int value) {
     if (key == 0) c->leaf_thresh = value;
     else if (key == 1) c->shade_thresh = value;
     else return fail(c, PT_E_ARG, "unknown tuning key");
+    drop_graph(c);
     return PT_OK;
 }
 
-int pt_render_async(pt_ctx* c, int frame_first, int n_frames, int acc_first) {
-    if (!c) return PT_E_ARG;
-    if (!c->scene_ok) return fail(c, PT_E_STATE, "pt_render before pt_upload_scene");
-    if (n_frames <= 0) return fail(c, PT_E_ARG, "n_frames must be > 0");
-    HIPCHK(c, hipSetDevice(c->cfg.device));
+// Enqueues one render launch (work-queue reset + kernel) on the context stream.  With
+// `frame_dev` the frame range is read on the device (progressive graph replay).
+static int enqueue_render(pt_ctx* c, int frame_first, int n_frames, int acc_first, const int* frame_dev,
+                          int frame_offset, bool events) {
     KParams p;
     std::memset(&p, 0, sizeof(p));
     p.sc.nodes = c->d_nodes;
@@ -1259,6 +1289,8 @@ int pt_render_async(pt_ctx* c, int frame_first, int n_frames, int acc_first) {
     p.frame_first = frame_first;
     p.n_frames = n_frames;
     p.acc_first = acc_first;
+    p.frame_dev = frame_dev;
+    p.frame_offset = frame_offset;
     p.max_bounce = c->cfg.max_bounce;
     p.mode = c->cfg.display_mode;
     p.flags = c->cfg.flags;
@@ -1279,17 +1311,19 @@ int pt_render_async(pt_ctx* c, int frame_first, int n_frames, int acc_first) {
     // 2 while-while persistent, 3 = 0 with the scene forced to stay in global memory
     bool use_lds = (c->variant == 0 || c->variant == 2) && c->lds_bytes <= kLdsSceneMax;
     if (c->variant != 1) HIPCHK(c, hipMemsetAsync(c->d_work, 0, sizeof(unsigned), c->stream));
-    hipEvent_t ev[2];
-    for (int i = 0; i < 2; i++) {
-        if (c->ev_free.empty()) {
-            HIPCHK(c, hipEventCreate(&ev[i]));
-        } else {
-            ev[i] = c->ev_free.back();
-            c->ev_free.pop_back();
+    hipEvent_t ev[2] = {nullptr, nullptr};
+    if (events) {
+        for (int i = 0; i < 2; i++) {
+            if (c->ev_free.empty()) {
+                HIPCHK(c, hipEventCreate(&ev[i]));
+            } else {
+                ev[i] = c->ev_free.back();
+                c->ev_free.pop_back();
+            }
         }
+        c->ev_pending.emplace_back(ev[0], ev[1]);
+        HIPCHK(c, hipEventRecord(ev[0], c->stream));
     }
-    c->ev_pending.emplace_back(ev[0], ev[1]);
-    HIPCHK(c, hipEventRecord(ev[0], c->stream));
     if (c->variant == 1) {
         dim3 grid((p.W + 15) / 16, (c->rows_local + 15) / 16);
         if (c->counting)
@@ -1323,8 +1357,80 @@ int pt_render_async(pt_ctx* c, int frame_first, int n_frames, int acc_first) {
 #undef PT_LAUNCH
     }
     HIPCHK(c, hipGetLastError());
-    HIPCHK(c, hipEventRecord(ev[1], c->stream));
+    if (events) HIPCHK(c, hipEventRecord(ev[1], c->stream));
     c->count_pending = c->counting;
+    return PT_OK;
+}
+
+int pt_render_async(pt_ctx* c, int frame_first, int n_frames, int acc_first) {
+    if (!c) return PT_E_ARG;
+    if (!c->scene_ok) return fail(c, PT_E_STATE, "pt_render before pt_upload_scene");
+    if (n_frames <= 0) return fail(c, PT_E_ARG, "n_frames must be > 0");
+    HIPCHK(c, hipSetDevice(c->cfg.device));
+    return enqueue_render(c, frame_first, n_frames, acc_first, nullptr, 0, true);
+}
+
+static void drop_graph(pt_ctx* c) {
+    if (c->graph_exec) (void)hipGraphExecDestroy(c->graph_exec);
+    if (c->graph) (void)hipGraphDestroy(c->graph);
+    c->graph_exec = nullptr;
+    c->graph = nullptr;
+}
+
+int pt_progressive_setup(pt_ctx* c, int frames_per_launch, int launches_per_replay) {
+    if (!c) return PT_E_ARG;
+    if (!c->scene_ok) return fail(c, PT_E_STATE, "pt_progressive_setup before pt_upload_scene");
+    if (frames_per_launch <= 0 || launches_per_replay <= 0) return fail(c, PT_E_ARG, "counts must be > 0");
+    if (c->counting) return fail(c, PT_E_STATE, "counting is not supported in graph replay");
+    HIPCHK(c, hipSetDevice(c->cfg.device));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    drop_graph(c);
+    if (!c->d_frame) HIPCHK(c, hipMalloc(&c->d_frame, 64));
+    HIPCHK(c, hipStreamBeginCapture(c->stream, hipStreamCaptureModeThreadLocal));
+    int rc = PT_OK;
+    for (int i = 0; i < launches_per_replay && rc == PT_OK; i++)
+        rc = enqueue_render(c, 0, frames_per_launch, 0, c->d_frame, i * frames_per_launch, false);
+    if (rc == PT_OK) {
+        hipLaunchKernelGGL(k_advance_frames, dim3(1), dim3(64), 0, c->stream, c->d_frame,
+                           frames_per_launch * launches_per_replay);
+    }
+    hipGraph_t g = nullptr;
+    hipError_t e = hipStreamEndCapture(c->stream, &g);
+    if (rc != PT_OK) { if (g) (void)hipGraphDestroy(g); return rc; }
+    if (e != hipSuccess) return fail(c, PT_E_HIP, std::string("hipStreamEndCapture: ") + hipGetErrorString(e));
+    c->graph = g;
+    HIPCHK(c, hipGraphInstantiate(&c->graph_exec, g, nullptr, nullptr, 0));
+    c->graph_frames = frames_per_launch * launches_per_replay;
+    return pt_progressive_reset(c, 1);
+}
+
+int pt_progressive_reset(pt_ctx* c, int next_frame) {
+    if (!c) return PT_E_ARG;
+    if (!c->d_frame) return fail(c, PT_E_STATE, "pt_progressive_setup first");
+    if (next_frame < 1) return fail(c, PT_E_ARG, "frames start at 1");
+    HIPCHK(c, hipMemcpyAsync(c->d_frame, &next_frame, sizeof(int), hipMemcpyHostToDevice, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    return PT_OK;
+}
+
+int pt_progressive_run(pt_ctx* c, int replays) {
+    if (!c) return PT_E_ARG;
+    if (!c->graph_exec) return fail(c, PT_E_STATE, "pt_progressive_setup first");
+    if (replays <= 0) return fail(c, PT_E_ARG, "replays must be > 0");
+    HIPCHK(c, hipSetDevice(c->cfg.device));
+    hipEvent_t ev[2];
+    for (int i = 0; i < 2; i++) {
+        if (c->ev_free.empty()) {
+            HIPCHK(c, hipEventCreate(&ev[i]));
+        } else {
+            ev[i] = c->ev_free.back();
+            c->ev_free.pop_back();
+        }
+    }
+    c->ev_pending.emplace_back(ev[0], ev[1]);
+    HIPCHK(c, hipEventRecord(ev[0], c->stream));
+    for (int r = 0; r < replays; r++) HIPCHK(c, hipGraphLaunch(c->graph_exec, c->stream));
+    HIPCHK(c, hipEventRecord(ev[1], c->stream));
     return PT_OK;
 }
 

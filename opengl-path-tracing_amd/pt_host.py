@@ -96,6 +96,9 @@ def lib():
             "pt_timing": (ip, [vp, C.POINTER(C.c_double), C.POINTER(ip), ip]),
             "pt_stats_ex": (ip, [vp, np.ctypeslib.ndpointer(np.uint64)]),
             "pt_set_tuning": (ip, [vp, ip, ip]),
+            "pt_progressive_setup": (ip, [vp, ip, ip]),
+            "pt_progressive_reset": (ip, [vp, ip]),
+            "pt_progressive_run": (ip, [vp, ip]),
         }
         for name, (res, args) in sig.items():
             fn = getattr(L, name)
@@ -296,6 +299,18 @@ class PathTracer:
         p, n = C.c_void_p(), C.c_size_t()
         self._check(lib().pt_accum_device(self.h, C.byref(p), C.byref(n)))
         return p.value, n.value
+
+    def progressive_setup(self, frames_per_launch, launches_per_replay):
+        """Capture the progressive sample loop as a hipGraph (see pt_api.h)."""
+        self._check(lib().pt_progressive_setup(self.h, int(frames_per_launch), int(launches_per_replay)))
+
+    def progressive_reset(self, next_frame=1):
+        self._check(lib().pt_progressive_reset(self.h, int(next_frame)))
+
+    def progressive_run(self, replays=1, sync=True):
+        self._check(lib().pt_progressive_run(self.h, int(replays)))
+        if sync:
+            self.sync()
 
     def diag(self):
         """Lane utilisation per kernel phase from the last counting render."""

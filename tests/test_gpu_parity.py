@@ -185,6 +185,27 @@ def test_large_scene_bitwise(big_scene, variant):
     assert_bitwise(got, want, "large scene")
 
 
+def test_progressive_graph_replay(cornell_scene, V):
+    """hipGraph-captured sample loop with a device frame counter == pt_render(1, N, 0)."""
+    pt = H.PathTracer(40, 24, max_bounce=8)
+    pt.set_kernel(V)
+    pt.upload(cornell_scene)
+    pt.render(1, 12, 0)
+    want = pt.read_rgba32f()
+    pt.write_rgba32f(np.full((24, 40, 4), np.nan, np.float32))   # frame 1 must overwrite
+    pt.progressive_setup(frames_per_launch=2, launches_per_replay=3)
+    pt.progressive_run(replays=2)
+    got = pt.read_rgba32f()
+    # a camera change drops the graph; re-setup and restart from frame 1
+    pt.set_camera(cornell_scene["cam"])
+    pt.progressive_setup(frames_per_launch=4, launches_per_replay=1)
+    pt.progressive_run(replays=3)
+    got2 = pt.read_rgba32f()
+    pt.close()
+    assert_bitwise(got, want, "graph replay")
+    assert_bitwise(got2, want, "graph replay after re-setup")
+
+
 def test_aces_epilogue(cornell_scene):
     pt = H.PathTracer(64, 64, max_bounce=5)
     pt.upload(cornell_scene)
