@@ -116,9 +116,12 @@ int pt_timing(pt_ctx* ctx, double* total_kernel_ms, int* n_launches, int reset);
 
 /* Kernel variant selection (0 = default/fastest); see DESIGN.md §5 for the list. */
 int pt_set_kernel(pt_ctx* ctx, int variant);
-/* Wave-scheduling thresholds of the state-machine kernel (lanes, 1..64):
- * key 0 = run the leaf phase once this many lanes wait at leaves,
- * key 1 = run the shading phase once this many lanes finished their segment. */
+/* Scheduling knobs of the state-machine kernel:
+ * key 0 = run the leaf phase once this many lanes wait at leaves (1..64, 0 = auto),
+ * key 1 = run the shading phase once this many lanes finished their segment (1..64, 0 = auto),
+ * key 2 = adaptive tile order (1 default: 8x8 tiles are queued most-expensive-first using
+ *         the segment counts of the previous renders; 0 = raster order).
+ * None of these change the image (each pixel's frames stay in order in one lane). */
 int pt_set_tuning(pt_ctx* ctx, int key, int value);
 
 #ifdef __cplusplus

@@ -53,6 +53,8 @@ struct KParams {
     int leaf_thresh, shade_thresh; // wave scheduling thresholds of the state-machine kernel
     const int* frame_dev;          // progressive graph: device frame counter (null = use frame_first)
     int frame_offset;              // this launch's frame offset from *frame_dev
+    const unsigned* tile_perm;     // queue order of 8x8 tiles (null = raster order)
+    unsigned* tile_cost;           // per-tile segment counts of this launch (null = off)
 };
 
 // Progressive mode (hipGraph replay): the frame range comes from a device counter, and
@@ -745,6 +747,7 @@ __global__ __launch_bounds__(256, MINW) void k_render_sm(KParams p) {
     int lx = -1, y = 0;
     int aidx = 0;             // rows_local * W < 2^31 (checked at pt_create)
     int k = 0, r = 0, bounce = 0;
+    unsigned tile_id = 0, pcost = 0;    // adaptive queue order: this pixel's tile + segments
     float4 acc = make_float4(0, 0, 0, 0);
     f3 psum = mk(0, 0, 0), o = mk(0, 0, 0), d = mk(0, 0, 1), inc = mk(0, 0, 0), col = mk(1, 1, 1);
     uint32_t state = 0;
@@ -764,6 +767,7 @@ __global__ __launch_bounds__(256, MINW) void k_render_sm(KParams p) {
             // ---------------- SHADE: finish segment, regenerate, set up next segment
             if (st == ST_SHADE && !fresh) {
                 if (COUNT) { c.seg++; if (hit) c.hits++; diag_tick(c.sw, c.sl); }
+                pcost++;
                 bool finished = false;
                 f3 rgb = inc;
                 if (hit && pt::length(col) > 0.01f) {
@@ -831,6 +835,7 @@ __global__ __launch_bounds__(256, MINW) void k_render_sm(KParams p) {
             }
             if (st == ST_SHADE && need_ray && lx >= 0 && k >= p.n_frames) {
                 p.accum[aidx] = acc;
+                if (p.tile_cost) atomicAdd(&p.tile_cost[tile_id], pcost);
                 lx = -1;
             }
             // wave-aggregated pull from the pixel queue
@@ -847,6 +852,7 @@ __global__ __launch_bounds__(256, MINW) void k_render_sm(KParams p) {
                         st = ST_DONE;
                     } else {
                         unsigned tile = id >> 6, w = id & 63u;
+                        if (p.tile_perm) tile = p.tile_perm[tile];
                         int cx = (int)(tile % (unsigned)tiles_x) * 8 + (int)(w & 7u);
                         int crow = (int)(tile / (unsigned)tiles_x) * 8 + (int)(w >> 3);
                         int cy = p.row0 + crow * p.row_stride;
@@ -854,6 +860,8 @@ __global__ __launch_bounds__(256, MINW) void k_render_sm(KParams p) {
                             lx = cx;
                             y = cy;
                             aidx = crow * p.W + cx;
+                            tile_id = tile;
+                            pcost = 0;
                             k = 0;
                             r = 0;
                             psum = mk(0, 0, 0);
@@ -999,6 +1007,12 @@ struct pt_ctx {
     unsigned long long* d_counters = nullptr;
     unsigned int* d_work = nullptr;
     int* d_frame = nullptr;                      // progressive graph frame counter
+    // adaptive queue order ("longest first"): per-tile segment counts measured by the
+    // previous renders order the next render's 8x8 tiles so cheap tiles form the tail
+    unsigned* d_tile_cost = nullptr;
+    unsigned* d_tile_perm = nullptr;
+    int n_tiles = 0;
+    bool adaptive = true, cost_pending = false;
     hipGraph_t graph = nullptr;
     hipGraphExec_t graph_exec = nullptr;
     int graph_frames = 0;
@@ -1068,6 +1082,15 @@ int pt_create(const pt_config* cfg, pt_ctx** out) {
     int n_cu = 0;
     HIPCHK(c, hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, cfg->device));
     c->persist_blocks = (unsigned)std::max(1, n_cu) * 8u;   // 8 x 256 threads = 32 waves per CU
+    c->n_tiles = ((cfg->width + 7) / 8) * ((c->rows_local + 7) / 8);
+    {
+        std::vector<unsigned> ident(std::max(c->n_tiles, 1));
+        for (size_t i = 0; i < ident.size(); i++) ident[i] = (unsigned)i;
+        HIPCHK(c, hipMalloc(&c->d_tile_perm, ident.size() * sizeof(unsigned)));
+        HIPCHK(c, hipMalloc(&c->d_tile_cost, ident.size() * sizeof(unsigned)));
+        HIPCHK(c, hipMemcpy(c->d_tile_perm, ident.data(), ident.size() * sizeof(unsigned), hipMemcpyHostToDevice));
+        HIPCHK(c, hipMemset(c->d_tile_cost, 0, ident.size() * sizeof(unsigned)));
+    }
     // default camera (ogl_path_trace.h:53-54)
     const float defcam[12] = {0, -6, 1, 0, 0, 1, 0, 0, 0, 0, 0, 0};
     pt_set_camera(c, defcam);
@@ -1081,6 +1104,8 @@ void pt_destroy(pt_ctx* c) {
     free_scene(c);
     (void)hipFree(c->accum); (void)hipFree(c->rgba8); (void)hipFree(c->d_counters); (void)hipFree(c->d_work);
     (void)hipFree(c->d_frame);
+    (void)hipFree(c->d_tile_perm);
+    (void)hipFree(c->d_tile_cost);
     for (auto& pr : c->ev_pending) { c->ev_free.push_back(pr.first); c->ev_free.push_back(pr.second); }
     for (hipEvent_t e : c->ev_free) (void)hipEventDestroy(e);
     if (c->stream) (void)hipStreamDestroy(c->stream);
@@ -1260,6 +1285,15 @@ int pt_set_tuning(pt_ctx* c, int key, int value) {
     if (value < 0 || value > 64) return fail(c, PT_E_ARG, "threshold must be in 1..64 (0 = automatic)");
     if (key == 0) c->leaf_thresh = value;
     else if (key == 1) c->shade_thresh = value;
+    else if (key == 2) {
+        c->adaptive = value != 0;
+        if (!c->adaptive && c->n_tiles > 0) {       // back to raster order
+            std::vector<unsigned> ident(c->n_tiles);
+            for (int i = 0; i < c->n_tiles; i++) ident[i] = (unsigned)i;
+            HIPCHK(c, hipMemcpy(c->d_tile_perm, ident.data(), ident.size() * sizeof(unsigned), hipMemcpyHostToDevice));
+            c->cost_pending = false;
+        }
+    }
     else return fail(c, PT_E_ARG, "unknown tuning key");
     drop_graph(c);
     return PT_OK;
@@ -1305,6 +1339,9 @@ static int enqueue_render(pt_ctx* c, int frame_first, int n_frames, int acc_firs
         p.leaf_thresh = c->leaf_thresh ? c->leaf_thresh : (lds_scene ? 32 : 8);
         p.shade_thresh = c->shade_thresh ? c->shade_thresh : (lds_scene ? 48 : 32);
     }
+    p.tile_perm = c->d_tile_perm;
+    p.tile_cost = (c->adaptive && !c->counting) ? c->d_tile_cost : nullptr;
+    if (p.tile_cost) c->cost_pending = true;
     if (c->counting) HIPCHK(c, hipMemsetAsync(c->d_counters, 0, 16 * sizeof(unsigned long long), c->stream));
     if (c->rows_local == 0) return PT_OK;
     // variants: 0 state-machine persistent (default), 1 one-lane-per-pixel tiles,
@@ -1430,6 +1467,7 @@ int pt_progressive_run(pt_ctx* c, int replays) {
     c->ev_pending.emplace_back(ev[0], ev[1]);
     HIPCHK(c, hipEventRecord(ev[0], c->stream));
     for (int r = 0; r < replays; r++) HIPCHK(c, hipGraphLaunch(c->graph_exec, c->stream));
+    if (c->adaptive && (c->variant == 0 || c->variant == 3)) c->cost_pending = true;
     HIPCHK(c, hipEventRecord(ev[1], c->stream));
     return PT_OK;
 }
@@ -1450,6 +1488,23 @@ int pt_sync(pt_ctx* c) {
     if (c->count_pending) {
         HIPCHK(c, hipMemcpy(c->last_counts, c->d_counters, 16 * sizeof(unsigned long long), hipMemcpyDeviceToHost));
         c->count_pending = false;
+    }
+    if (c->cost_pending && c->n_tiles > 1) {
+        // longest-processing-time-first order of the 8x8 tiles for the next renders: a
+        // bucket sort on the measured segment counts, raster order inside a bucket
+        std::vector<unsigned> cost(c->n_tiles), perm(c->n_tiles);
+        HIPCHK(c, hipMemcpy(cost.data(), c->d_tile_cost, c->n_tiles * sizeof(unsigned), hipMemcpyDeviceToHost));
+        unsigned mx = 1;
+        for (unsigned v : cost) mx = std::max(mx, v);
+        const int nb = 1024;
+        std::vector<int> cnt(nb + 1, 0);
+        auto bucket = [&](unsigned v) { return nb - 1 - (int)((unsigned long long)v * (nb - 1) / mx); };
+        for (unsigned v : cost) cnt[bucket(v) + 1]++;
+        for (int b = 0; b < nb; b++) cnt[b + 1] += cnt[b];
+        for (int t = 0; t < c->n_tiles; t++) perm[cnt[bucket(cost[t])]++] = (unsigned)t;
+        HIPCHK(c, hipMemcpy(c->d_tile_perm, perm.data(), c->n_tiles * sizeof(unsigned), hipMemcpyHostToDevice));
+        HIPCHK(c, hipMemset(c->d_tile_cost, 0, c->n_tiles * sizeof(unsigned)));
+        c->cost_pending = false;
     }
     return PT_OK;
 }

@@ -262,11 +262,13 @@ class PathTracer:
     def set_kernel(self, variant):
         self._check(lib().pt_set_kernel(self.h, int(variant)))
 
-    def set_tuning(self, leaf_thresh=None, shade_thresh=None):
+    def set_tuning(self, leaf_thresh=None, shade_thresh=None, adaptive=None):
         if leaf_thresh is not None:
             self._check(lib().pt_set_tuning(self.h, 0, int(leaf_thresh)))
         if shade_thresh is not None:
             self._check(lib().pt_set_tuning(self.h, 1, int(shade_thresh)))
+        if adaptive is not None:
+            self._check(lib().pt_set_tuning(self.h, 2, int(bool(adaptive))))
 
     def dispatch(self, frame, accumulate):
         """One glDispatchCompute with uniforms frame/accumulate (ogl_path_trace.h:176-183)."""

@@ -206,6 +206,20 @@ def test_progressive_graph_replay(cornell_scene, V):
     assert_bitwise(got2, want, "graph replay after re-setup")
 
 
+def test_adaptive_tile_order_is_invisible(cornell_scene):
+    """The longest-first tile order learnt from earlier renders changes only the schedule."""
+    imgs = []
+    for adaptive in (0, 1):
+        pt = H.PathTracer(72, 40, max_bounce=8)
+        pt.set_tuning(adaptive=adaptive)
+        pt.upload(cornell_scene)
+        for f0 in (1, 3, 5):
+            pt.render(f0, 2, 0 if f0 == 1 else 1)
+        imgs.append(pt.read_rgba32f())
+        pt.close()
+    assert_bitwise(imgs[1], imgs[0], "adaptive order")
+
+
 def test_aces_epilogue(cornell_scene):
     pt = H.PathTracer(64, 64, max_bounce=5)
     pt.upload(cornell_scene)

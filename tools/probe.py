@@ -36,8 +36,8 @@ def main():
     def apply(v, tu):
         pt.set_kernel(v)
         if tu != "-":
-            lt, stt = tu.split(":")
-            pt.set_tuning(int(lt), int(stt))
+            parts = [int(x) for x in tu.split(":")]
+            pt.set_tuning(parts[0], parts[1], parts[2] if len(parts) > 2 else 1)
 
     for v, c, tu in configs:
         apply(v, tu)
