@@ -835,7 +835,7 @@ __global__ __launch_bounds__(256, MINW) void k_render_sm(KParams p) {
             }
             if (st == ST_SHADE && need_ray && lx >= 0 && k >= p.n_frames) {
                 p.accum[aidx] = acc;
-                if (p.tile_cost) atomicAdd(&p.tile_cost[tile_id], pcost);
+                if (p.tile_cost && tile_id != ~0u) atomicAdd(&p.tile_cost[tile_id], pcost);
                 lx = -1;
             }
             // wave-aggregated pull from the pixel queue
@@ -860,7 +860,9 @@ __global__ __launch_bounds__(256, MINW) void k_render_sm(KParams p) {
                             lx = cx;
                             y = cy;
                             aidx = crow * p.W + cx;
-                            tile_id = tile;
+                            // cost sample: 4 pixels per 8x8 tile report (one 64-B memory-side
+                            // atomic each), the rest keep tile_id = ~0u
+                            tile_id = ((w & 0x1bu) == 0u) ? tile : ~0u;
                             pcost = 0;
                             k = 0;
                             r = 0;
