@@ -262,13 +262,15 @@ class PathTracer:
     def set_kernel(self, variant):
         self._check(lib().pt_set_kernel(self.h, int(variant)))
 
-    def set_tuning(self, leaf_thresh=None, shade_thresh=None, adaptive=None):
+    def set_tuning(self, leaf_thresh=None, shade_thresh=None, adaptive=None, waves_per_simd=None):
         if leaf_thresh is not None:
             self._check(lib().pt_set_tuning(self.h, 0, int(leaf_thresh)))
         if shade_thresh is not None:
             self._check(lib().pt_set_tuning(self.h, 1, int(shade_thresh)))
         if adaptive is not None:
             self._check(lib().pt_set_tuning(self.h, 2, int(bool(adaptive))))
+        if waves_per_simd is not None:
+            self._check(lib().pt_set_tuning(self.h, 3, int(waves_per_simd)))
 
     def dispatch(self, frame, accumulate):
         """One glDispatchCompute with uniforms frame/accumulate (ogl_path_trace.h:176-183)."""

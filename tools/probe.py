@@ -37,7 +37,8 @@ def main():
         pt.set_kernel(v)
         if tu != "-":
             parts = [int(x) for x in tu.split(":")]
-            pt.set_tuning(parts[0], parts[1], parts[2] if len(parts) > 2 else 1)
+            pt.set_tuning(parts[0], parts[1], parts[2] if len(parts) > 2 else 1,
+                          parts[3] if len(parts) > 3 else 0)
 
     for v, c, tu in configs:
         apply(v, tu)
