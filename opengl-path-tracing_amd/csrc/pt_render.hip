@@ -330,7 +330,23 @@ struct SceneView {
     const float4* tris;
     const float4* mats;
     const float4* spheres;
+    int np, tp;    // plane strides (float4) of the state-machine kernel's LDS copy
 };
+
+// Node / triangle-record access of the state-machine kernel.  Global memory holds AoS
+// records (node = 2 float4, triangle slot = 4 float4).  Its LDS copy is split into
+// planes -- node half h of node i at [h*np + i], triangle quad k of slot s at [k*tp + s] --
+// so random per-lane gathers of one half/quad hit 16-B bank groups spread over all 64
+// banks instead of every 2nd (nodes, 32-B stride) or 4th (triangles, 64-B stride) group.
+template <bool LDS>
+__device__ __forceinline__ void node_at(const SceneView& S, int i, float4& lo, float4& hi) {
+    if (LDS) { lo = S.nodes[i]; hi = S.nodes[i + S.np]; }
+    else { lo = S.nodes[2 * i]; hi = S.nodes[2 * i + 1]; }
+}
+template <bool LDS>
+__device__ __forceinline__ float4 tri_quad(const SceneView& S, int slot, int k) {
+    return LDS ? S.tris[slot + k * S.tp] : S.tris[4 * slot + k];
+}
 
 __device__ __forceinline__ float qdiv(float a, float b, float rb) {
     float q = a * rb;
@@ -345,15 +361,15 @@ __device__ __forceinline__ bool in_guard(float v, float lo, float hi) {
 
 // Scalar on purpose: packed f32 (v_pk_fma_f32) takes two passes on gfx950's SIMD-32, so
 // it saves issue slots but no VALU cycles, and its broadcast operand pairs cost registers
-// (measured: no gain, spills).  `tn <= min(tf, t)` equals `tn <= tf && tn <= t` for the
-// finite quotients of the guarded path (t may be +inf).
+// (measured: no gain, spills).  t is compared, not folded into the min3: fminf on a
+// loop-carried value costs a canonicalizing v_max.
 __device__ __forceinline__ bool slab_fast(float4 A, float4 B, f3 o, f3 d, f3 rd, float cur_t) {
     float x0 = qdiv(A.x - o.x, d.x, rd.x), x1 = qdiv(A.y - o.x, d.x, rd.x);
     float y0 = qdiv(A.z - o.y, d.y, rd.y), y1 = qdiv(A.w - o.y, d.y, rd.y);
     float z0 = qdiv(B.x - o.z, d.z, rd.z), z1 = qdiv(B.y - o.z, d.z, rd.z);
     float tn = fmaxf(fmaxf(fminf(x0, x1), fminf(y0, y1)), fminf(z0, z1));
-    float tf = fminf(fminf(fmaxf(x0, x1), fmaxf(y0, y1)), fminf(fmaxf(z0, z1), cur_t));
-    return tn <= tf;
+    float tf = fminf(fminf(fmaxf(x0, x1), fmaxf(y0, y1)), fmaxf(z0, z1));
+    return tn <= tf && tn <= cur_t;
 }
 
 template <bool COUNT>
@@ -443,8 +459,10 @@ __device__ __forceinline__ float tri_hit_bf(const float4* T, f3 o, f3 d, float t
 // Same test, but the plane distance is computed first and the edge tests run only if some
 // lane of the wave still needs them (a wave-uniform skip; per lane the verdict is the
 // same select as tri_hit_bf, so the bits are identical).
-__device__ __forceinline__ float tri_hit_lazy(const float4* T, f3 o, f3 d, float tbest, f3& n) {
-    float4 q0 = T[0], q1 = T[1], q2 = T[2], q3 = T[3];
+template <bool LDS>
+__device__ __forceinline__ float tri_hit_lazy(const SceneView& S, int slot, f3 o, f3 d, float tbest, f3& n) {
+    float4 q0 = tri_quad<LDS>(S, slot, 0), q1 = tri_quad<LDS>(S, slot, 1);
+    float4 q2 = tri_quad<LDS>(S, slot, 2), q3 = tri_quad<LDS>(S, slot, 3);
     n = mk(q0.w, q1.w, q2.w);
     float t = -(pt::dot(n, o) + q3.x) / pt::dot(n, d);
     bool ok = !(t < 0.0f) && (t < tbest);
@@ -723,26 +741,26 @@ enum : int { ST_DONE = 0, ST_TRAV = 1, ST_LEAF = 2, ST_SHADE = 3 };
 // leaves or shade_thresh lanes wait to shade; lanes only ever leave TRAV here, so the two
 // separate counts are needed only once the waiting total reaches the smaller threshold.
 // ALL_FAST: every walking lane is inside the exact-reciprocal guard (wave-uniform).
-template <bool ALL_FAST, bool COUNT>
+// No step counter: the reference's `steps < numNodes` bound (:393) can never bind on an
+// accepted scene -- pt_upload_scene rejects link graphs with a cycle, and a walk in an
+// acyclic graph visits each node at most once.  The transition is select-only; `leaf`
+// keeps the raw link (~code), decoded in LEAF.
+template <bool ALL_FAST, bool COUNT, bool LDS>
 __device__ __forceinline__ void trav_walk(const SceneView& S, f3 o, f3 d, f3 rd, bool fast, float t,
-                                          int n_nodes, unsigned long long live, int leaf_thresh,
-                                          int shade_thresh, int& st, int& bi, int& leaf, int& steps,
-                                          Cnt& c) {
+                                          unsigned long long live, int leaf_thresh, int shade_thresh,
+                                          int& st, int& bi, int& leaf, Cnt& c) {
     const int min_thresh = leaf_thresh < shade_thresh ? leaf_thresh : shade_thresh;
     for (;;) {
         if (st == ST_TRAV) {
-            float4 lo = S.nodes[2 * bi], hi = S.nodes[2 * bi + 1];
+            float4 lo, hi;
+            node_at<LDS>(S, bi, lo, hi);
             int a = __float_as_int(hi.z), b = __float_as_int(hi.w);
             bool hb = (ALL_FAST || fast) ? slab_fast(lo, hi, o, d, rd, t) : slab(lo, hi, o, d, t);
             if (COUNT) { c.nodes++; diag_tick(c.tw, c.tl); }
-            steps++;
+            const bool to_leaf = hb && a < 0;
             bi = (hb && a >= 0) ? a : b;
-            if (hb && a < 0) {
-                leaf = ~a;
-                st = ST_LEAF;
-            } else if (bi < 0 || steps >= n_nodes) {
-                st = ST_SHADE;
-            }
+            leaf = a;
+            st = to_leaf ? ST_LEAF : (bi < 0 ? ST_SHADE : ST_TRAV);
         }
         unsigned long long mt = __ballot(st == ST_TRAV);
         if (!mt) break;
@@ -758,10 +776,11 @@ __global__ __launch_bounds__(256, MINW) void k_render_sm(KParams p) {
     resolve_frames(p);
     extern __shared__ float4 lds[];
     SceneView S;
-    if (LDS) {
-        int nn = 2 * p.sc.n_nodes, nt = 4 * p.n_slots, nm = 3 * p.n_mats, ns = 2 * p.sc.n_spheres;
-        for (int i = threadIdx.x; i < nn; i += blockDim.x) lds[i] = p.sc.nodes[i];
-        for (int i = threadIdx.x; i < nt; i += blockDim.x) lds[nn + i] = p.sc.tris[i];
+    if (LDS) {      // planes (see node_at / tri_quad)
+        const int N = p.sc.n_nodes, T = p.n_slots, nn = 2 * N, nt = 4 * T;
+        const int nm = 3 * p.n_mats, ns = 2 * p.sc.n_spheres;
+        for (int i = threadIdx.x; i < nn; i += blockDim.x) lds[(i & 1) * N + (i >> 1)] = p.sc.nodes[i];
+        for (int i = threadIdx.x; i < nt; i += blockDim.x) lds[nn + (i & 3) * T + (i >> 2)] = p.sc.tris[i];
         for (int i = threadIdx.x; i < nm; i += blockDim.x) lds[nn + nt + i] = p.sc.mats[i];
         for (int i = threadIdx.x; i < ns; i += blockDim.x) lds[nn + nt + nm + i] = p.sc.spheres[i];
         __syncthreads();
@@ -769,11 +788,14 @@ __global__ __launch_bounds__(256, MINW) void k_render_sm(KParams p) {
         S.tris = lds + nn;
         S.mats = lds + nn + nt;
         S.spheres = lds + nn + nt + nm;
+        S.np = N;
+        S.tp = T;
     } else {
         S.nodes = p.sc.nodes;
         S.tris = p.sc.tris;
         S.mats = p.sc.mats;
         S.spheres = p.sc.spheres;
+        S.np = S.tp = 0;
     }
     const int lane = threadIdx.x & 63;
     const f3 cpos = mk(p.cam[0], p.cam[1], p.cam[2]), cfwd = mk(p.cam[3], p.cam[4], p.cam[5]);
@@ -802,7 +824,7 @@ __global__ __launch_bounds__(256, MINW) void k_render_sm(KParams p) {
     bool fast = false;
     f3 rd = mk(0, 0, 0);
     float t = 0.0f;
-    int hprim = -1, bi = -1, leaf = 0, steps = 0;
+    int hprim = -1, bi = -1, leaf = 0;
 
     for (;;) {
         int nS = __popcll(__ballot(st == ST_SHADE));
@@ -822,9 +844,9 @@ __global__ __launch_bounds__(256, MINW) void k_render_sm(KParams p) {
                     f3 normal;
                     int mat;
                     if (hprim >= 0) {             // triangle: stored n, flipped (:421-428)
-                        const float4* T = S.tris + 4 * hprim;
-                        normal = mk(T[0].w, T[1].w, T[2].w);
-                        mat = __float_as_int(T[3].y);
+                        normal = mk(tri_quad<LDS>(S, hprim, 0).w, tri_quad<LDS>(S, hprim, 1).w,
+                                    tri_quad<LDS>(S, hprim, 2).w);
+                        mat = __float_as_int(tri_quad<LDS>(S, hprim, 3).y);
                     } else {                      // sphere: normalize(hit - center) (:380)
                         const int si = -2 - hprim;
                         float4 s0 = S.spheres[2 * si];
@@ -974,7 +996,6 @@ __global__ __launch_bounds__(256, MINW) void k_render_sm(KParams p) {
                     }
                 }
                 fresh = false;
-                steps = 0;
                 bi = use_tris ? 0 : -1;
                 st = use_tris ? ST_TRAV : ST_SHADE;
             }
@@ -982,17 +1003,18 @@ __global__ __launch_bounds__(256, MINW) void k_render_sm(KParams p) {
             // ---------------- LEAF: both triangle tests + the 2-way choice (:406-429)
             if (st == ST_LEAF) {
                 if (COUNT) { c.tri += 2; diag_tick(c.lw, c.ll); }
-                const float4* T0 = S.tris + 8 * (leaf >> 1);
+                const int code = ~leaf;                      // (slot << 1) | single
+                const int s0 = code & ~1;                    // slots 2k, 2k+1
                 f3 n0, n1;
-                float h1 = tri_hit_lazy(T0, o, d, t, n0);
-                float h2 = tri_hit_lazy(T0 + 4, o, d, t, n1);
+                float h1 = tri_hit_lazy<LDS>(S, s0, o, d, t, n0);
+                float h2 = tri_hit_lazy<LDS>(S, s0 + 1, o, d, t, n1);
                 bool c1 = h1 > 0.0001f && h1 < t && (h1 < h2 || h2 < 0.0001f);
                 bool c2 = !c1 && h2 > 0.0001f && h2 < t;
                 if (c1 || c2) {
                     t = c1 ? h1 : h2;
-                    hprim = (leaf & ~1) + (c1 ? 0 : 1);      // slots 2k, 2k+1
+                    hprim = s0 + (c1 ? 0 : 1);
                 }
-                st = (bi > -1 && steps < n_nodes) ? ST_TRAV : ST_SHADE;
+                st = bi > -1 ? ST_TRAV : ST_SHADE;
             }
         } else {
             // ---------------- TRAV: walk until a leaf is hit / the chain ends; yield to the
@@ -1001,11 +1023,11 @@ __global__ __launch_bounds__(256, MINW) void k_render_sm(KParams p) {
             // the per-node IEEE-division branch.
             const unsigned long long live = __ballot(st != ST_DONE);
             if (__all(fast || st != ST_TRAV))
-                trav_walk<true, COUNT>(S, o, d, rd, fast, t, n_nodes, live, p.leaf_thresh, p.shade_thresh,
-                                       st, bi, leaf, steps, c);
+                trav_walk<true, COUNT, LDS>(S, o, d, rd, fast, t, live, p.leaf_thresh, p.shade_thresh, st, bi,
+                                       leaf, c);
             else
-                trav_walk<false, COUNT>(S, o, d, rd, fast, t, n_nodes, live, p.leaf_thresh, p.shade_thresh,
-                                        st, bi, leaf, steps, c);
+                trav_walk<false, COUNT, LDS>(S, o, d, rd, fast, t, live, p.leaf_thresh, p.shade_thresh, st, bi,
+                                        leaf, c);
         }
     }
     flush_counters<COUNT>(p, c);
@@ -1184,7 +1206,9 @@ int pt_upload_scene(pt_ctx* c, const float* tris, int n_tris, const float* bvh, 
             return fail(c, PT_E_SCENE, "internal node without a hit link at node " + std::to_string(i));
         }
     }
-    // acyclicity of the (hit, miss) link graph reachable from node 0
+    // acyclicity of the (hit, miss) link graph reachable from node 0.  The state-machine
+    // kernel relies on it: a walk then visits each node at most once, so the reference's
+    // steps < numNodes bound (:393) cannot bind and no step counter is kept.
     if (n_nodes > 0) {
         std::vector<unsigned char> color(n_nodes, 0);
         std::vector<std::pair<int, int>> st;
@@ -1328,7 +1352,7 @@ int pt_set_tuning(pt_ctx* c, int key, int value) {
     if (key == 0) c->leaf_thresh = value;
     else if (key == 1) c->shade_thresh = value;
     else if (key == 3) {
-        if (value != 0 && value != 5 && value != 6) return fail(c, PT_E_ARG, "waves per SIMD must be 5 or 6 (0 = auto)");
+        if (value != 0 && (value < 5 || value > 8)) return fail(c, PT_E_ARG, "waves per SIMD must be 5..8 (0 = auto)");
         c->minw = value;
     }
     else if (key == 2) {
@@ -1382,7 +1406,7 @@ static int enqueue_render(pt_ctx* c, int frame_first, int n_frames, int acc_firs
     p.scene_fast = c->scene_fast;
     {
         bool lds_scene = c->lds_bytes <= kLdsSceneMax && c->variant != 3;
-        p.leaf_thresh = c->leaf_thresh ? c->leaf_thresh : (lds_scene ? 32 : 8);
+        p.leaf_thresh = c->leaf_thresh ? c->leaf_thresh : (lds_scene ? 32 : 16);
         p.shade_thresh = c->shade_thresh ? c->shade_thresh : (lds_scene ? 48 : 32);
     }
     p.tile_perm = c->d_tile_perm;
@@ -1425,10 +1449,12 @@ static int enqueue_render(pt_ctx* c, int frame_first, int n_frames, int acc_firs
     else hipLaunchKernelGGL((K<false, L, MW>), grid, dim3(256), L ? lds : 0, c->stream, p);
         // occupancy: 6 waves/SIMD (80 VGPRs) measured best for LDS scenes (+5% on C2 over 5),
         // a tie for global-memory scenes
-        const bool w6 = c->minw ? c->minw == 6 : use_lds;
+        const int mw = c->minw ? c->minw : 6;
 #define PT_LAUNCH_SM(L, M)                                                                                    \
     if (c->counting) hipLaunchKernelGGL((k_render_sm<true, L, 5, M>), grid, dim3(256), L ? lds : 0, c->stream, p); \
-    else if (w6) hipLaunchKernelGGL((k_render_sm<false, L, 6, M>), grid, dim3(256), L ? lds : 0, c->stream, p); \
+    else if (mw == 8) hipLaunchKernelGGL((k_render_sm<false, L, 8, M>), grid, dim3(256), L ? lds : 0, c->stream, p); \
+    else if (mw == 7) hipLaunchKernelGGL((k_render_sm<false, L, 7, M>), grid, dim3(256), L ? lds : 0, c->stream, p); \
+    else if (mw == 6) hipLaunchKernelGGL((k_render_sm<false, L, 6, M>), grid, dim3(256), L ? lds : 0, c->stream, p); \
     else hipLaunchKernelGGL((k_render_sm<false, L, 5, M>), grid, dim3(256), L ? lds : 0, c->stream, p);
         if (c->variant == 0 || c->variant == 3) {
             bool multi = p.rpp > 1;

@@ -24,7 +24,8 @@ import subprocess
 import numpy as np
 
 PKG_DIR = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(PKG_DIR, "build", "libptrace.so")
+# PT_LIB selects another in-tree build of the same library (tools/ab.py A/B timing only).
+LIB_PATH = os.environ.get("PT_LIB") or os.path.join(PKG_DIR, "build", "libptrace.so")
 INCLUDE_DIR = os.path.join(os.path.dirname(PKG_DIR), "include")
 
 PT_FLAG_NO_AA, PT_FLAG_NO_SKY, PT_FLAG_NO_SPHERES, PT_FLAG_NO_TRIANGLES, PT_FLAG_REF_DISPATCH = 1, 2, 4, 8, 16
