@@ -185,12 +185,18 @@ def main():
     achieved = bytes_per_launch / (avg_launch_ms * 1e-3) / 1e9
 
     traffic = None
+    valu = None
     try:
         with open(args.traffic_json) as fh:
             tj = json.load(fh)
         if (tj.get("width"), tj.get("height"), tj.get("chunk"), tj.get("scene")) == (W, H, chunk, scene) \
                 and world == 1:
             traffic = tj.get("hbm_bytes_per_launch")
+            if tj.get("valu_busy_frac") is not None:
+                valu = {"busy_frac": round(tj["valu_busy_frac"], 4),
+                        "active_lanes_per_instr": round(tj.get("valu_active_lanes_per_instr", 0.0), 2),
+                        "source": "PMC (tools/gpu_pmc.sh -> tools/pmc_traffic.py): SQ_INSTS_VALU x 2 cycles "
+                                  "/ (1024 SIMDs x GRBM_GUI_ACTIVE/8) -- the bound that actually binds"}
     except (OSError, ValueError):
         pass
 
@@ -229,7 +235,7 @@ def main():
                          "basis": "algorithmic bytes (SURVEY.md §8(d)) per launch / avg launch time (HIP events "
                                   "on the render stream, %d launches); the scene is cache/LDS-resident so frac "
                                   "can exceed 1; traffic = PMC HBM bytes per launch (profiles/)" % n_launch,
-                         "avg_launch_ms": round(avg_launch_ms, 3)},
+                         "avg_launch_ms": round(avg_launch_ms, 3), "valu": valu},
             "cpu_baseline": cpu,
         }
         print(json.dumps(line), flush=True)

@@ -1082,8 +1082,8 @@ struct pt_ctx {
     int n_nodes = 0, n_spheres = 0, n_mats = 0, n_slots = 0, scene_fast = 0;
     size_t lds_bytes = 0;
     unsigned persist_blocks = 2048;
-    // 0 = automatic: 32/48 when the scene is staged in LDS (best on C2), 8/32 when the walk
-    // reads global memory (latency-bound; best on the C3/C4 stand-ins) -- tools/probe.py sweeps
+    // 0 = automatic: 32/48 when the scene is staged in LDS (best on C2), 16/32 when the walk
+    // reads global memory (latency-bound; best on the C3 stand-in) -- tools/probe.py sweeps
     int leaf_thresh = 0, shade_thresh = 0, minw = 0;
     bool scene_ok = false, cam_ok = false, counting = false;
     float cam[12] = {0};

@@ -55,6 +55,12 @@ def main():
         out["hbm_bytes_per_launch"] = 2 * avg["FETCH_SIZE"] * 1024 + avg["WRITE_SIZE"] * 1024
     if "SQ_THREAD_CYCLES_VALU" in avg:
         out["valu_active_lanes_per_instr"] = avg["SQ_THREAD_CYCLES_VALU"] / max(avg["SQ_ACTIVE_INST_VALU"], 1)
+    if "SQ_INSTS_VALU" in avg and "GRBM_GUI_ACTIVE" in avg:
+        # VALU pipe occupancy: a wave64 VALU op holds a SIMD-32 for 2 cycles (MI355X_MICROARCH.md);
+        # GRBM_GUI_ACTIVE sums the 8 XCDs' busy clocks; 256 CUs x 4 SIMDs.
+        cycles = avg["GRBM_GUI_ACTIVE"] / 8.0
+        out["valu_busy_frac"] = 2.0 * avg["SQ_INSTS_VALU"] / (1024.0 * cycles)
+        out["clock_ghz"] = cycles / (avg.get("launch_ms_sq2", avg.get("launch_ms_sq1", 1.0)) * 1e6)
     if "SQ_WAVE_CYCLES" in avg and "SQ_WAIT_ANY" in avg:
         tot = avg["SQ_WAVE_CYCLES"]
         out["wave_cycle_split"] = {k: avg[k] / tot for k in ("SQ_ACTIVE_INST_ANY", "SQ_WAIT_INST_ANY", "SQ_WAIT_ANY") if k in avg}
