@@ -57,6 +57,12 @@ struct KParams {
     int frame_offset;              // this launch's frame offset from *frame_dev
     const unsigned* tile_perm;     // queue order of 8x8 tiles (null = raster order)
     unsigned* tile_cost;           // per-tile segment counts of this launch (null = off)
+    // frame-split work items (state-machine kernel): a queue item is (pixel, `group`
+    // consecutive frames); with rgb != null the lane stores each frame's pixel colour to
+    // rgb[pixel * n_frames + k] and k_accum_frames applies the running mean in frame order.
+    // group = n_frames and rgb = null: the lane owns all frames and accumulates in registers.
+    int group;
+    float4* rgb;
 };
 
 // Progressive mode (hipGraph replay): the frame range comes from a device counter, and
@@ -734,6 +740,7 @@ __global__ __launch_bounds__(256, MINW) void k_render_wave(KParams p) {
 // next node, same t), so results are bit-identical; only lane interleaving changes.
 // =====================================================================================
 enum : int { ST_DONE = 0, ST_TRAV = 1, ST_LEAF = 2, ST_SHADE = 3 };
+constexpr unsigned kPullBatch = 32;
 
 // The TRAV phase: each TRAV lane advances one node per iteration (bvh_intersect + the link
 // choice of calculateRayCollision :389-431) until it stops at a leaf whose box it hit
@@ -771,7 +778,7 @@ __device__ __forceinline__ void trav_walk(const SceneView& S, f3 o, f3 d, f3 rd,
     }
 }
 
-template <bool COUNT, bool LDS, int MINW, bool MULTI>
+template <bool COUNT, bool LDS, int MINW, bool MULTI, bool SPLIT>
 __global__ __launch_bounds__(256, MINW) void k_render_sm(KParams p) {
     resolve_frames(p);
     extern __shared__ float4 lds[];
@@ -801,7 +808,8 @@ __global__ __launch_bounds__(256, MINW) void k_render_sm(KParams p) {
     const f3 cpos = mk(p.cam[0], p.cam[1], p.cam[2]), cfwd = mk(p.cam[3], p.cam[4], p.cam[5]);
     const f3 cright = mk(p.cam[6], p.cam[7], p.cam[8]), cup = mk(p.cam[9], p.cam[10], p.cam[11]);
     const int tiles_x = (p.W + 7) >> 3;
-    const unsigned total_ids = (unsigned)tiles_x * (unsigned)((p.rows_local + 7) >> 3) * 64u;
+    const unsigned n_groups = SPLIT ? (unsigned)((p.n_frames + p.group - 1) / p.group) : 1u;
+    const unsigned total_ids = (unsigned)tiles_x * (unsigned)((p.rows_local + 7) >> 3) * n_groups * 64u;
     const int n_nodes = p.sc.n_nodes;
     const bool use_tris = !(p.flags & PT_FLAG_NO_TRIANGLES) && n_nodes > 0;
 
@@ -811,7 +819,8 @@ __global__ __launch_bounds__(256, MINW) void k_render_sm(KParams p) {
     bool need_ray = true;     // next SHADE must start a new camera ray
     int lx = -1, y = 0;
     int aidx = 0;             // rows_local * W < 2^31 (checked at pt_create)
-    int k = 0, r = 0, bounce = 0;
+    int k = 0, kend = 0, r = 0, bounce = 0;   // frames k..kend-1 of this work item
+    unsigned qnext = 0, qend = 0;             // wave's reserved queue ids (frame-split mode)
     unsigned tile_id = 0, pcost = 0;    // adaptive queue order: this pixel's tile + segments
     float4 acc = make_float4(0, 0, 0, 0);
     f3 psum = mk(0, 0, 0), o = mk(0, 0, 0), d = mk(0, 0, 1), inc = mk(0, 0, 0), col = mk(1, 1, 1);
@@ -897,43 +906,69 @@ __global__ __launch_bounds__(256, MINW) void k_render_sm(KParams p) {
                 }
                 need_ray = finished;
                 if (finished) {
+                    bool frame_done = true;
+                    f3 px;
                     if (MULTI) {          // raysPerPixel > 1: pixel = 0 + sum of rays, / rpp
                         psum = psum + rgb;
                         r++;
-                        if (r >= p.rpp) {
+                        frame_done = r >= p.rpp;
+                        px = psum / (float)p.rpp;
+                    } else {              // raysPerPixel == 1: pixel = (0 + rgb) / 1
+                        px = (mk(0, 0, 0) + rgb) / 1.0f;
+                    }
+                    if (frame_done) {
+                        if (SPLIT) {
+                            p.rgb[(size_t)aidx * (size_t)p.n_frames + (size_t)k] = make_float4(px.x, px.y, px.z, 0.0f);
+                        } else {
                             int f = p.frame_first + k;
-                            acc = accumulate(acc, psum / (float)p.rpp, f, k > 0 || p.acc_first == 1);
+                            acc = accumulate(acc, px, f, k > 0 || p.acc_first == 1);
+                        }
+                        if (MULTI) {
                             psum = mk(0, 0, 0);
                             r = 0;
-                            k++;
                         }
-                    } else {              // raysPerPixel == 1: pixel = (0 + rgb) / 1
-                        int f = p.frame_first + k;
-                        acc = accumulate(acc, (mk(0, 0, 0) + rgb) / 1.0f, f, k > 0 || p.acc_first == 1);
                         k++;
                     }
                 }
                 fresh = true;
             }
-            if (st == ST_SHADE && need_ray && lx >= 0 && k >= p.n_frames) {
-                p.accum[aidx] = acc;
+            if (st == ST_SHADE && need_ray && lx >= 0 && k >= (SPLIT ? kend : p.n_frames)) {
+                if (!SPLIT) p.accum[aidx] = acc;
                 if (p.tile_cost && tile_id != ~0u) atomicAdd(&p.tile_cost[tile_id], pcost);
                 lx = -1;
             }
-            // wave-aggregated pull from the pixel queue
+            // wave-aggregated pull from the work queue.  Frame-split items are short, so
+            // there a wave reserves ids in batches of kPullBatch (one queue atomic per
+            // batch instead of per pull; the counter is one address for the whole chip).
             bool want = st == ST_SHADE && lx < 0;
             unsigned long long m = __ballot(want);
             if (m) {
-                int leader = __ffsll((long long)m) - 1;
-                unsigned base = 0;
-                if (lane == leader) base = atomicAdd(p.work_counter, (unsigned)__popcll(m));
-                base = __shfl(base, leader, 64);
+                const unsigned need = (unsigned)__popcll(m);
+                const unsigned rank = (unsigned)__popcll(m & ((1ull << lane) - 1ull));
+                const int leader = __ffsll((long long)m) - 1;
+                unsigned id;
+                if (SPLIT && qend - qnext >= need) {
+                    id = qnext + rank;
+                    qnext += need;
+                } else {
+                    const unsigned avail = SPLIT ? qend - qnext : 0u;
+                    const unsigned take = SPLIT ? max(need - avail, kPullBatch) : need;
+                    unsigned base = 0;
+                    if (lane == leader) base = atomicAdd(p.work_counter, take);
+                    base = __shfl(base, leader, 64);
+                    id = rank < avail ? qnext + rank : base + (rank - avail);
+                    if (SPLIT) {
+                        qnext = base + (need - avail);
+                        qend = base + take;
+                    }
+                }
                 if (want) {
-                    unsigned id = base + (unsigned)__popcll(m & ((1ull << lane) - 1ull));
                     if (id >= total_ids) {
                         st = ST_DONE;
                     } else {
-                        unsigned tile = id >> 6, w = id & 63u;
+                        const unsigned item = id >> 6, w = id & 63u;
+                        unsigned tile = SPLIT ? item / n_groups : item;
+                        const int g = SPLIT ? (int)(item - tile * n_groups) : 0;
                         if (p.tile_perm) tile = p.tile_perm[tile];
                         int cx = (int)(tile % (unsigned)tiles_x) * 8 + (int)(w & 7u);
                         int crow = (int)(tile / (unsigned)tiles_x) * 8 + (int)(w >> 3);
@@ -946,10 +981,11 @@ __global__ __launch_bounds__(256, MINW) void k_render_sm(KParams p) {
                             // atomic each), the rest keep tile_id = ~0u
                             tile_id = ((w & 0x1bu) == 0u) ? tile : ~0u;
                             pcost = 0;
-                            k = 0;
+                            k = g * p.group;
+                            if (SPLIT) kend = min(k + p.group, p.n_frames);
                             r = 0;
                             psum = mk(0, 0, 0);
-                            acc = p.acc_first ? p.accum[aidx] : make_float4(0, 0, 0, 0);
+                            if (!SPLIT) acc = p.acc_first ? p.accum[aidx] : make_float4(0, 0, 0, 0);
                             need_ray = true;
                         }
                     }
@@ -1033,6 +1069,25 @@ __global__ __launch_bounds__(256, MINW) void k_render_sm(KParams p) {
     flush_counters<COUNT>(p, c);
 }
 
+// Running mean of the frame-split mode (:548-551): per local pixel, the launch's frames in
+// order from the per-frame colours the render kernel stored -- the same accumulate() the
+// lane applies in registers otherwise.  Pixels outside the dispatch footprint are skipped.
+__global__ __launch_bounds__(256) void k_accum_frames(KParams p) {
+    resolve_frames(p);
+    const long long n = (long long)p.rows_local * p.W;
+    const long long idx = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (idx >= n) return;
+    const int crow = (int)(idx / p.W), cx = (int)(idx - (long long)crow * p.W);
+    if (cx >= p.x_limit || p.row0 + crow * p.row_stride >= p.y_limit) return;
+    float4 acc = p.acc_first ? p.accum[idx] : make_float4(0, 0, 0, 0);
+    const float4* src = p.rgb + (size_t)idx * (size_t)p.n_frames;
+    for (int k = 0; k < p.n_frames; k++) {
+        float4 v = src[k];
+        acc = accumulate(acc, mk(v.x, v.y, v.z), p.frame_first + k, k > 0 || p.acc_first == 1);
+    }
+    p.accum[idx] = acc;
+}
+
 // ACES film tonemap epilogue (screenQuadFrag.c:12-26) -> RGBA8, alpha 255.
 __global__ __launch_bounds__(256) void k_aces(const float4* __restrict__ src, uchar4* __restrict__ dst,
                                               long long n) {
@@ -1085,6 +1140,11 @@ struct pt_ctx {
     // 0 = automatic: 32/48 when the scene is staged in LDS (best on C2), 16/32 when the walk
     // reads global memory (latency-bound; best on the C3 stand-in) -- tools/probe.py sweeps
     int leaf_thresh = 0, shade_thresh = 0, minw = 0;
+    // frame-split work items (KParams::group): 0 = automatic, n = frames per item
+    int group_force = 0;
+    int n_cu = 0;
+    float4* d_rgb = nullptr;       // per-(pixel, frame) colours of the frame-split mode
+    size_t rgb_bytes = 0;
     bool scene_ok = false, cam_ok = false, counting = false;
     float cam[12] = {0};
     int variant = 0;
@@ -1145,6 +1205,7 @@ int pt_create(const pt_config* cfg, pt_ctx** out) {
     int n_cu = 0;
     HIPCHK(c, hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, cfg->device));
     c->persist_blocks = (unsigned)std::max(1, n_cu) * 8u;   // 8 x 256 threads = 32 waves per CU
+    c->n_cu = std::max(1, n_cu);
     c->n_tiles = ((cfg->width + 7) / 8) * ((c->rows_local + 7) / 8);
     {
         std::vector<unsigned> ident(std::max(c->n_tiles, 1));
@@ -1169,6 +1230,7 @@ void pt_destroy(pt_ctx* c) {
     (void)hipFree(c->d_frame);
     (void)hipFree(c->d_tile_perm);
     (void)hipFree(c->d_tile_cost);
+    (void)hipFree(c->d_rgb);
     for (auto& pr : c->ev_pending) { c->ev_free.push_back(pr.first); c->ev_free.push_back(pr.second); }
     for (hipEvent_t e : c->ev_free) (void)hipEventDestroy(e);
     if (c->stream) (void)hipStreamDestroy(c->stream);
@@ -1348,11 +1410,17 @@ int pt_set_kernel(pt_ctx* c, int variant) {
 
 int pt_set_tuning(pt_ctx* c, int key, int value) {
     if (!c) return PT_E_ARG;
+    if (key == 5) {
+        if (value < 0) return fail(c, PT_E_ARG, "frames per work item must be >= 1 (0 = automatic)");
+        c->group_force = value;
+        drop_graph(c);
+        return PT_OK;
+    }
     if (value < 0 || value > 64) return fail(c, PT_E_ARG, "threshold must be in 1..64 (0 = automatic)");
     if (key == 0) c->leaf_thresh = value;
     else if (key == 1) c->shade_thresh = value;
     else if (key == 3) {
-        if (value != 0 && (value < 5 || value > 8)) return fail(c, PT_E_ARG, "waves per SIMD must be 5..8 (0 = auto)");
+        if (value != 0 && value != 5 && value != 6) return fail(c, PT_E_ARG, "waves per SIMD must be 5 or 6 (0 = auto)");
         c->minw = value;
     }
     else if (key == 2) {
@@ -1366,6 +1434,37 @@ int pt_set_tuning(pt_ctx* c, int key, int value) {
     }
     else return fail(c, PT_E_ARG, "unknown tuning key");
     drop_graph(c);
+    return PT_OK;
+}
+
+// Frames per work item of the state-machine kernel (KParams::group).  Items of a few frames
+// keep every resident lane busy to the end of a launch and let the per-GPU share of a
+// multi-GPU split (fewer pixels than lanes at 1080p/8) use the whole chip; the per-frame
+// colours go to a buffer and k_accum_frames applies the running mean in frame order.
+// Measured (C2 scene, 64-frame launches): 8 frames per item +6% over whole-pixel items on
+// one GPU, 2-4 frames +85% on a 1080p/8 share; so ~16 items per resident lane, capped at
+// 8 frames.  group == n_frames is the register mode (a lane owns all frames of a pixel and
+// accumulates in registers); the counting build always uses it.
+static int plan_group(const pt_ctx* c, int n_frames) {
+    if ((c->variant != 0 && c->variant != 3) || c->counting) return n_frames;
+    if (c->group_force > 0) return std::min(c->group_force, n_frames);
+    const int waves = c->minw ? c->minw : 6;
+    const double lanes = (double)c->n_cu * 4.0 * waves * 64.0;
+    const double px = (double)c->rows_local * c->cfg.width;
+    const bool lds_scene = c->lds_bytes <= kLdsSceneMax && c->variant != 3;
+    int g = (int)(px * n_frames / (16.0 * lanes));
+    g = std::max(1, std::min(g, lds_scene ? 8 : 4));   // C3 stand-in: 4 frames +8% over 8
+    return std::min(g, n_frames);
+}
+
+static int ensure_rgb(pt_ctx* c, int n_frames) {
+    size_t need = (size_t)std::max(c->rows_local, 1) * (size_t)c->cfg.width * (size_t)n_frames * sizeof(float4);
+    if (need <= c->rgb_bytes) return PT_OK;
+    (void)hipFree(c->d_rgb);
+    c->d_rgb = nullptr;
+    c->rgb_bytes = 0;
+    HIPCHK(c, hipMalloc(&c->d_rgb, need));
+    c->rgb_bytes = need;
     return PT_OK;
 }
 
@@ -1409,6 +1508,12 @@ static int enqueue_render(pt_ctx* c, int frame_first, int n_frames, int acc_firs
         p.leaf_thresh = c->leaf_thresh ? c->leaf_thresh : (lds_scene ? 32 : 16);
         p.shade_thresh = c->shade_thresh ? c->shade_thresh : (lds_scene ? 48 : 32);
     }
+    p.group = plan_group(c, n_frames);
+    if (p.group < n_frames) {
+        int rc = ensure_rgb(c, n_frames);
+        if (rc) return rc;
+        p.rgb = c->d_rgb;
+    }
     p.tile_perm = c->d_tile_perm;
     p.tile_cost = (c->adaptive && !c->counting) ? c->d_tile_cost : nullptr;
     if (p.tile_cost) c->cost_pending = true;
@@ -1442,7 +1547,8 @@ static int enqueue_render(pt_ctx* c, int frame_first, int n_frames, int acc_firs
         // queue empty and exit.  Never more blocks than 8x8 tiles (64 lanes per tile).
         size_t lds = use_lds ? c->lds_bytes : 0;
         unsigned tiles = (unsigned)(((p.W + 7) / 8) * ((c->rows_local + 7) / 8));
-        unsigned blocks = std::min<unsigned>(c->persist_blocks, std::max(1u, (tiles + 3) / 4));
+        unsigned items = tiles * (unsigned)((n_frames + p.group - 1) / p.group);   // 64-lane items
+        unsigned blocks = std::min<unsigned>(c->persist_blocks, std::max(1u, (items + 3) / 4));
         dim3 grid(blocks);
 #define PT_LAUNCH(K, L, MW)                                                                                   \
     if (c->counting) hipLaunchKernelGGL((K<true, L, MW>), grid, dim3(256), L ? lds : 0, c->stream, p);        \
@@ -1451,11 +1557,11 @@ static int enqueue_render(pt_ctx* c, int frame_first, int n_frames, int acc_firs
         // a tie for global-memory scenes
         const int mw = c->minw ? c->minw : 6;
 #define PT_LAUNCH_SM(L, M)                                                                                    \
-    if (c->counting) hipLaunchKernelGGL((k_render_sm<true, L, 5, M>), grid, dim3(256), L ? lds : 0, c->stream, p); \
-    else if (mw == 8) hipLaunchKernelGGL((k_render_sm<false, L, 8, M>), grid, dim3(256), L ? lds : 0, c->stream, p); \
-    else if (mw == 7) hipLaunchKernelGGL((k_render_sm<false, L, 7, M>), grid, dim3(256), L ? lds : 0, c->stream, p); \
-    else if (mw == 6) hipLaunchKernelGGL((k_render_sm<false, L, 6, M>), grid, dim3(256), L ? lds : 0, c->stream, p); \
-    else hipLaunchKernelGGL((k_render_sm<false, L, 5, M>), grid, dim3(256), L ? lds : 0, c->stream, p);
+    if (c->counting) hipLaunchKernelGGL((k_render_sm<true, L, 5, M, false>), grid, dim3(256), L ? lds : 0, c->stream, p); \
+    else if (p.rgb && mw == 6) hipLaunchKernelGGL((k_render_sm<false, L, 6, M, true>), grid, dim3(256), L ? lds : 0, c->stream, p); \
+    else if (p.rgb) hipLaunchKernelGGL((k_render_sm<false, L, 5, M, true>), grid, dim3(256), L ? lds : 0, c->stream, p); \
+    else if (mw == 6) hipLaunchKernelGGL((k_render_sm<false, L, 6, M, false>), grid, dim3(256), L ? lds : 0, c->stream, p); \
+    else hipLaunchKernelGGL((k_render_sm<false, L, 5, M, false>), grid, dim3(256), L ? lds : 0, c->stream, p);
         if (c->variant == 0 || c->variant == 3) {
             bool multi = p.rpp > 1;
             if (use_lds && multi) { PT_LAUNCH_SM(true, true) }
@@ -1468,6 +1574,10 @@ static int enqueue_render(pt_ctx* c, int frame_first, int n_frames, int acc_firs
             else { PT_LAUNCH(k_render_wave, false, 1) }
         }
 #undef PT_LAUNCH
+        if (p.rgb) {
+            long long px = (long long)c->rows_local * p.W;
+            hipLaunchKernelGGL(k_accum_frames, dim3((unsigned)((px + 255) / 256)), dim3(256), 0, c->stream, p);
+        }
     }
     HIPCHK(c, hipGetLastError());
     if (events) HIPCHK(c, hipEventRecord(ev[1], c->stream));
@@ -1499,6 +1609,10 @@ int pt_progressive_setup(pt_ctx* c, int frames_per_launch, int launches_per_repl
     HIPCHK(c, hipStreamSynchronize(c->stream));
     drop_graph(c);
     if (!c->d_frame) HIPCHK(c, hipMalloc(&c->d_frame, 64));
+    if (plan_group(c, frames_per_launch) < frames_per_launch) {   // no allocation inside the capture
+        int rc0 = ensure_rgb(c, frames_per_launch);
+        if (rc0) return rc0;
+    }
     HIPCHK(c, hipStreamBeginCapture(c->stream, hipStreamCaptureModeThreadLocal));
     int rc = PT_OK;
     for (int i = 0; i < launches_per_replay && rc == PT_OK; i++)

@@ -263,7 +263,7 @@ class PathTracer:
     def set_kernel(self, variant):
         self._check(lib().pt_set_kernel(self.h, int(variant)))
 
-    def set_tuning(self, leaf_thresh=None, shade_thresh=None, adaptive=None, waves_per_simd=None):
+    def set_tuning(self, leaf_thresh=None, shade_thresh=None, adaptive=None, waves_per_simd=None, group=None):
         if leaf_thresh is not None:
             self._check(lib().pt_set_tuning(self.h, 0, int(leaf_thresh)))
         if shade_thresh is not None:
@@ -272,6 +272,8 @@ class PathTracer:
             self._check(lib().pt_set_tuning(self.h, 2, int(bool(adaptive))))
         if waves_per_simd is not None:
             self._check(lib().pt_set_tuning(self.h, 3, int(waves_per_simd)))
+        if group is not None:
+            self._check(lib().pt_set_tuning(self.h, 5, int(group)))
 
     def dispatch(self, frame, accumulate):
         """One glDispatchCompute with uniforms frame/accumulate (ogl_path_trace.h:176-183)."""

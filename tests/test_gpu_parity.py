@@ -246,3 +246,42 @@ def test_aces_epilogue(cornell_scene):
     rgba8 = pt.read_rgba8()
     pt.close()
     assert np.array_equal(rgba8, O.aces_rgba8(img))
+
+
+@pytest.mark.parametrize("group", [1, 3, 64])
+@pytest.mark.parametrize("rpp", [1, 3])
+@pytest.mark.parametrize("variant", [0, 3])
+def test_frame_split_work_items(cornell_scene, group, rpp, variant):
+    """Frame-split work items (tuning key 5): a pixel's frames spread over several lanes,
+    per-frame colours stored and the running mean applied in frame order by k_accum_frames.
+    Covers accumulate onto a prior image, a frame offset and 64 = the register mode."""
+    prior = np.random.default_rng(3).random((30, 44, 4), dtype=np.float32)
+    want = O.render(cornell_scene, 44, 30, max_bounce=8, frame_first=7, n_frames=7, acc_first=1,
+                    accum=prior.copy(), rpp=rpp)
+    pt = H.PathTracer(44, 30, max_bounce=8, rays_per_pixel=rpp)
+    pt.set_kernel(variant)
+    pt.set_tuning(group=group)
+    pt.upload(cornell_scene)
+    pt.write_rgba32f(prior)
+    pt.render(7, 7, 1)
+    got = pt.read_rgba32f()
+    pt.close()
+    assert_bitwise(got, want, "group %d rpp %d variant %d" % (group, rpp, variant))
+
+
+def test_frame_split_footprint_and_graph(cornell_scene):
+    """Frame-split mode with the REF_DISPATCH footprint (k_accum_frames must not touch
+    pixels outside it) and inside a captured progressive graph."""
+    got = gpu_render(cornell_scene, 256, 256, mode=1, n_frames=3, flags=H.PT_FLAG_REF_DISPATCH)
+    assert np.all(got[250:] == 0) and np.all(got[:, 250:] == 0)
+    want = O.render(cornell_scene, 256, 256, mode=1, n_frames=3)
+    assert_bitwise(got[:250, :250], want[:250, :250], "footprint, split")
+    want = O.render(cornell_scene, 40, 24, max_bounce=6, n_frames=12)
+    pt = H.PathTracer(40, 24, max_bounce=6)
+    pt.set_tuning(group=2)
+    pt.upload(cornell_scene)
+    pt.progressive_setup(frames_per_launch=4, launches_per_replay=3)
+    pt.progressive_run(replays=1)
+    got = pt.read_rgba32f()
+    pt.close()
+    assert_bitwise(got, want, "graph, split")

@@ -25,10 +25,11 @@ def main():
     ap.add_argument("--width", type=int, default=1920)
     ap.add_argument("--height", type=int, default=1080)
     ap.add_argument("--bounces", type=int, default=8)
-    ap.add_argument("--tunings", default="24:40", help="leaf:shade thresholds for variants 6/7, comma list")
+    ap.add_argument("--tunings", default="0:0", help="leaf:shade[:adaptive[:waves[:group]]] for variants 0/3, comma list")
+    ap.add_argument("--world", type=int, default=1, help="render rank 0 of a WORLD-way row split (per-GPU share)")
     a = ap.parse_args()
     sb = pt_host.setupBuffers(*pt_scenes.write_scene(a.scene, os.path.join(REPO, "scenes")))
-    pt = pt_host.PathTracer(a.width, a.height, max_bounce=a.bounces)
+    pt = pt_host.PathTracer(a.width, a.height, max_bounce=a.bounces, rank=0, world=a.world)
     pt.upload(sb)
     seg = {}
     configs = [(int(v), int(c), tu) for v in a.variants.split(",") for c in a.chunks.split(",")
@@ -38,7 +39,7 @@ def main():
         if tu != "-":
             parts = [int(x) for x in tu.split(":")]
             pt.set_tuning(parts[0], parts[1], parts[2] if len(parts) > 2 else 1,
-                          parts[3] if len(parts) > 3 else 0)
+                          parts[3] if len(parts) > 3 else 0, parts[4] if len(parts) > 4 else None)
 
     for v, c, tu in configs:
         apply(v, tu)
