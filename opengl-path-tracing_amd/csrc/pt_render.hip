@@ -59,7 +59,9 @@ struct KParams {
     unsigned* tile_cost;           // per-tile segment counts of this launch (null = off)
     // frame-split work items (state-machine kernel): a queue item is (pixel, `group`
     // consecutive frames); with rgb != null the lane stores each frame's pixel colour to
-    // rgb[pixel * n_frames + k] and k_accum_frames applies the running mean in frame order.
+    // rgb[k * pixels + pixel] (frame planes: the accumulate pass reads coalesced, and the
+    // 8 lanes on one tile row write one 128-B line) and k_accum_frames applies the running
+    // mean in frame order.
     // group = n_frames and rgb = null: the lane owns all frames and accumulates in registers.
     int group;
     float4* rgb;
@@ -918,7 +920,8 @@ __global__ __launch_bounds__(256, MINW) void k_render_sm(KParams p) {
                     }
                     if (frame_done) {
                         if (SPLIT) {
-                            p.rgb[(size_t)aidx * (size_t)p.n_frames + (size_t)k] = make_float4(px.x, px.y, px.z, 0.0f);
+                            p.rgb[(size_t)k * (size_t)(p.rows_local * p.W) + (size_t)aidx] =
+                                make_float4(px.x, px.y, px.z, 0.0f);
                         } else {
                             int f = p.frame_first + k;
                             acc = accumulate(acc, px, f, k > 0 || p.acc_first == 1);
@@ -1080,9 +1083,9 @@ __global__ __launch_bounds__(256) void k_accum_frames(KParams p) {
     const int crow = (int)(idx / p.W), cx = (int)(idx - (long long)crow * p.W);
     if (cx >= p.x_limit || p.row0 + crow * p.row_stride >= p.y_limit) return;
     float4 acc = p.acc_first ? p.accum[idx] : make_float4(0, 0, 0, 0);
-    const float4* src = p.rgb + (size_t)idx * (size_t)p.n_frames;
+    const float4* src = p.rgb + idx;
     for (int k = 0; k < p.n_frames; k++) {
-        float4 v = src[k];
+        float4 v = src[(size_t)k * (size_t)n];
         acc = accumulate(acc, mk(v.x, v.y, v.z), p.frame_first + k, k > 0 || p.acc_first == 1);
     }
     p.accum[idx] = acc;
