@@ -12,7 +12,7 @@ import pt_host  # noqa: E402
 import pt_scenes  # noqa: E402
 
 ap = argparse.ArgumentParser()
-ap.add_argument("--chunk", type=int, default=64)
+ap.add_argument("--chunk", type=int, default=128)
 ap.add_argument("--launches", type=int, default=2)
 ap.add_argument("--variant", type=int, default=0)
 ap.add_argument("--scene", default="cornell")

@@ -1,10 +1,12 @@
-"""Reduce rocprofv3 PMC passes (tools/gpu_pmc.sh output) for the render kernel.
+"""Reduce rocprofv3 PMC passes (tools/gpu_pmc.sh output) for the render launch.
 
-Writes profiles/<tag>_pmc.json and profiles/traffic_latest.json:
+A render launch is the state-machine kernel plus, in the frame-split mode, the k_accum_frames
+pass that follows it; counters are summed over both and averaged over launches (the first,
+warm-up launch dropped).  Writes profiles/<tag>_pmc.json and profiles/traffic_latest.json:
   hbm_bytes_per_launch = 2 * FETCH_SIZE * 1024 + WRITE_SIZE * 1024, per render launch.
 The factor 2 on FETCH_SIZE is the gfx950 correction of MI355X_MICROARCH.md §HBM (FETCH_SIZE
-reports half the bytes of wide 16-B/lane reads; the accumulator reads are float4 per lane);
-WRITE_SIZE is exact for 16-B/lane stores.  Raw values are kept alongside.
+reports half the bytes of wide 16-B/lane reads; the accumulator and colour-buffer reads are
+float4 per lane); WRITE_SIZE is exact for 16-B/lane stores.  Raw values are kept alongside.
 """
 import collections
 import csv
@@ -16,22 +18,34 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 def load(d):
+    """-> list of launches: (summed counters, {kernel kind: duration ms})."""
     path = os.path.join(d, "run_counter_collection.csv")
-    agg = collections.defaultdict(lambda: collections.defaultdict(float))
-    dur = {}
+    disp = collections.OrderedDict()
     for r in csv.DictReader(open(path)):
-        if "k_render" not in r["Kernel_Name"]:
+        name = r["Kernel_Name"]
+        kind = "render" if "k_render" in name else ("accum" if "k_accum_frames" in name else None)
+        if kind is None:
             continue
         key = int(r["Dispatch_Id"])
-        agg[key][r["Counter_Name"]] += float(r["Counter_Value"])
-        dur[key] = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) * 1e-6
-    return agg, dur
+        e = disp.setdefault(key, {"kind": kind, "ctr": collections.defaultdict(float), "ms": 0.0})
+        e["ctr"][r["Counter_Name"]] += float(r["Counter_Value"])
+        e["ms"] = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) * 1e-6
+    launches = []
+    for key in sorted(disp):
+        e = disp[key]
+        if e["kind"] == "render" or not launches:
+            launches.append((collections.defaultdict(float), {}))
+        ctr, ms = launches[-1]
+        for cn, v in e["ctr"].items():
+            ctr[cn] += v
+        ms[e["kind"]] = ms.get(e["kind"], 0.0) + e["ms"]
+    return launches
 
 
 def main():
     pmc = sys.argv[1] if len(sys.argv) > 1 else os.path.join(REPO, "gpurun_out", "pmc")
     tag = sys.argv[2] if len(sys.argv) > 2 else "latest"
-    meta = dict(scene="cornell", width=1920, height=1080, chunk=64)
+    meta = dict(scene="cornell", width=1920, height=1080, chunk=128)
     for a in sys.argv[3:]:
         k, v = a.split("=")
         meta[k] = int(v) if v.isdigit() else v
@@ -41,12 +55,13 @@ def main():
         d = os.path.join(pmc, name)
         if not os.path.isdir(d) or not os.path.exists(os.path.join(d, "run_counter_collection.csv")):
             continue
-        agg, dur = load(d)
-        keys = sorted(agg)[1:] or sorted(agg)          # drop the warm-up launch when possible
-        for k in keys:
-            for cn, v in agg[k].items():
+        launches = load(d)
+        for ctr, ms in (launches[1:] or launches):     # drop the warm-up launch when possible
+            for cn, v in ctr.items():
                 per[cn].append(v)
-            per["launch_ms_" + name].append(dur[k])
+            per["launch_ms_" + name].append(sum(ms.values()))
+            for kind, v in ms.items():
+                per["%s_ms_%s" % (kind, name)].append(v)
     avg = {k: sum(v) / len(v) for k, v in per.items()}
     out["counters_per_launch"] = avg
     if "FETCH_SIZE" in avg and "WRITE_SIZE" in avg:
