@@ -34,8 +34,8 @@ HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
 # scene, W, H, spp, bounces, frames per launch, graph launches/replay
 CONFIGS = {
     "C2": ("cornell", 1920, 1080, 1024, 8, 128, 0),
-    "C3": ("bunny", 1920, 1080, 256, 8, 32, 0),
-    "C4": ("sponza", 1920, 1080, 256, 8, 32, 0),
+    "C3": ("bunny", 1920, 1080, 256, 8, 256, 0),
+    "C4": ("sponza", 1920, 1080, 256, 8, 256, 0),
     "C5": ("cornell", 3840, 2160, 4096, 8, 64, 8),
 }
 

@@ -108,7 +108,8 @@ int pt_stats(pt_ctx* ctx, double* kernel_ms, unsigned long long out[5]);
 /* Counting-build diagnostics of the last render: out[0..4] as pt_stats, then per kernel
  * phase (traversal step, leaf test, segment) the wave iterations and the active lanes
  * summed over them: [5] trav waves, [6] trav lanes, [7] leaf waves, [8] leaf lanes,
- * [9] segment waves, [10] segment lanes (persistent kernels; 0 for the tiled kernel). */
+ * [9] segment waves, [10] segment lanes (persistent kernels; 0 for the tiled kernel),
+ * [11] segments outside the exact-reciprocal guard (state-machine kernel). */
 int pt_stats_ex(pt_ctx* ctx, unsigned long long out[16]);
 /* Sum of render-kernel durations (HIP events on the render stream) and the number of
  * launches since the last reset; reset != 0 clears both after reading. */

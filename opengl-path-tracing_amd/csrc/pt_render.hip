@@ -86,8 +86,10 @@ struct Cnt {
     // counting-build diagnostics: per phase, wave iterations (counted once per wave by the
     // first active lane) and active lanes summed over those iterations
     uint32_t tw, tl, lw, ll, sw, sl;
+    uint32_t slow;   // segments outside the exact-reciprocal guard (IEEE-division walk)
+    uint32_t nan;    // segments whose ray has a NaN component (can never hit)
 };
-constexpr int kNumCounters = 11;
+constexpr int kNumCounters = 13;
 
 // Records one wave iteration of a phase: the first active lane adds 1 and popcount(exec).
 __device__ __forceinline__ void diag_tick(uint32_t& waves, uint32_t& lanes) {
@@ -138,6 +140,16 @@ __device__ __forceinline__ float tri_hit(const float4* T, f3 o, f3 d, float tbes
     return t;
 }
 
+// A ray with a NaN component in o or d can never hit: every triangle distance
+// -(dot(n,o)+d0)/dot(n,d) and every sphere root is NaN, and NaN fails the `t < tbest` /
+// `ht > 0.0001` acceptance tests (:297, :378, :411-428).  Its walk still visits up to every
+// node -- a single lane crawling the whole tree (60-70 ms on the 69k-triangle stand-in,
+// the tail of its launch) -- so the render kernels skip the walk; its result (no hit, t =
+// +inf) is the reference's.  Counting builds still walk, to count the node visits.
+__device__ __forceinline__ bool ray_has_nan(f3 o, f3 d) {
+    return o.x != o.x || o.y != o.y || o.z != o.z || d.x != d.x || d.y != d.y || d.z != d.z;
+}
+
 // calculateRayCollision (computeShader.c:367-432)
 template <bool COUNT>
 __device__ __forceinline__ bool collide(const KParams& p, f3 o, f3 d, f3& normal, f3& hitp,
@@ -167,6 +179,7 @@ __device__ __forceinline__ bool collide(const KParams& p, f3 o, f3 d, f3& normal
         }
     }
     if ((p.flags & PT_FLAG_NO_TRIANGLES) || p.sc.n_nodes <= 0) return hit;
+    if (!COUNT && ray_has_nan(o, d)) return hit;
     int bi = 0;
     for (int steps = 0; bi > -1 && steps < p.sc.n_nodes; steps++) {
         float4 lo = p.sc.nodes[2 * bi], hi = p.sc.nodes[2 * bi + 1];
@@ -275,6 +288,16 @@ __device__ __forceinline__ float4 accumulate(float4 prev, f3 rgb, int frame, boo
                        prev.w * w + 1.0f / ff);
 }
 
+// Non-temporal 16-B accesses (streamed data that must not evict the scene from L2/MALL).
+typedef float nt_f4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ void nt_store(float4* dst, float4 v) {
+    __builtin_nontemporal_store(nt_f4{v.x, v.y, v.z, v.w}, reinterpret_cast<nt_f4*>(dst));
+}
+__device__ __forceinline__ float4 nt_load(const float4* src) {
+    nt_f4 v = __builtin_nontemporal_load(reinterpret_cast<const nt_f4*>(src));
+    return make_float4(v.x, v.y, v.z, v.w);
+}
+
 __device__ __forceinline__ unsigned long long wave_sum(unsigned long long v) {
     for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
     return v;
@@ -283,7 +306,8 @@ __device__ __forceinline__ unsigned long long wave_sum(unsigned long long v) {
 template <bool COUNT>
 __device__ __forceinline__ void flush_counters(const KParams& p, const Cnt& c) {
     if (!COUNT) return;
-    unsigned long long v[kNumCounters] = {c.seg, c.nodes, c.tri, c.sph, c.hits, c.tw, c.tl, c.lw, c.ll, c.sw, c.sl};
+    unsigned long long v[kNumCounters] = {c.seg, c.nodes, c.tri, c.sph, c.hits, c.tw, c.tl, c.lw, c.ll, c.sw, c.sl,
+                                          c.slow, c.nan};
     for (int i = 0; i < kNumCounters; i++) {
         unsigned long long s = wave_sum(v[i]);
         if ((threadIdx.x & 63) == 0) atomicAdd(&p.counters[i], s);
@@ -409,6 +433,7 @@ __device__ __forceinline__ bool collide_v(const SceneView& S, int n_nodes, int n
         }
     }
     if ((flags & PT_FLAG_NO_TRIANGLES) || n_nodes <= 0) return hit;
+    if (!COUNT && ray_has_nan(o, d)) return hit;
     int bi = 0;
     for (int steps = 0; bi > -1 && steps < n_nodes; steps++) {
         float4 lo = S.nodes[2 * bi], hi = S.nodes[2 * bi + 1];
@@ -518,7 +543,7 @@ __device__ __forceinline__ bool collide_ww(const SceneView& S, int n_nodes, int 
             }
         }
     }
-    int bi = (active && !(flags & PT_FLAG_NO_TRIANGLES) && n_nodes > 0) ? 0 : -1;
+    int bi = (active && !(flags & PT_FLAG_NO_TRIANGLES) && n_nodes > 0 && (COUNT || !ray_has_nan(o, d))) ? 0 : -1;
     int steps = 0;
     int leaf = 0;
     bool pend = false;
@@ -920,8 +945,10 @@ __global__ __launch_bounds__(256, MINW) void k_render_sm(KParams p) {
                     }
                     if (frame_done) {
                         if (SPLIT) {
-                            p.rgb[(size_t)k * (size_t)(p.rows_local * p.W) + (size_t)aidx] =
-                                make_float4(px.x, px.y, px.z, 0.0f);
+                            // streamed once, read once by k_accum_frames: non-temporal, so the
+                            // colour stream does not evict the scene from L2/MALL
+                            nt_store(p.rgb + (size_t)k * (size_t)(p.rows_local * p.W) + (size_t)aidx,
+                                     make_float4(px.x, px.y, px.z, 0.0f));
                         } else {
                             int f = p.frame_first + k;
                             acc = accumulate(acc, px, f, k > 0 || p.acc_first == 1);
@@ -1016,6 +1043,8 @@ __global__ __launch_bounds__(256, MINW) void k_render_sm(KParams p) {
                        in_guard(o.z, 0x1p-40f, 0x1p60f) && in_guard(d.x, 0x1p-20f, 2.0f) && d.x != 0.0f &&
                        in_guard(d.y, 0x1p-20f, 2.0f) && d.y != 0.0f && in_guard(d.z, 0x1p-20f, 2.0f) && d.z != 0.0f;
                 if (fast) rd = mk(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
+                if (COUNT && !fast) c.slow++;
+                if (COUNT && ray_has_nan(o, d)) c.nan++;
                 t = __builtin_huge_valf();
                 hprim = -1;
                 if (!(p.flags & PT_FLAG_NO_SPHERES)) {
@@ -1035,8 +1064,9 @@ __global__ __launch_bounds__(256, MINW) void k_render_sm(KParams p) {
                     }
                 }
                 fresh = false;
-                bi = use_tris ? 0 : -1;
-                st = use_tris ? ST_TRAV : ST_SHADE;
+                const bool walk = use_tris && (COUNT || !ray_has_nan(o, d));
+                bi = walk ? 0 : -1;
+                st = walk ? ST_TRAV : ST_SHADE;
             }
         } else if (nL > 0 && (nL >= p.leaf_thresh || nT == 0)) {
             // ---------------- LEAF: both triangle tests + the 2-way choice (:406-429)
@@ -1085,7 +1115,7 @@ __global__ __launch_bounds__(256) void k_accum_frames(KParams p) {
     float4 acc = p.acc_first ? p.accum[idx] : make_float4(0, 0, 0, 0);
     const float4* src = p.rgb + idx;
     for (int k = 0; k < p.n_frames; k++) {
-        float4 v = src[(size_t)k * (size_t)n];
+        float4 v = nt_load(src + (size_t)k * (size_t)n);
         acc = accumulate(acc, mk(v.x, v.y, v.z), p.frame_first + k, k > 0 || p.acc_first == 1);
     }
     p.accum[idx] = acc;

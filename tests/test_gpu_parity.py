@@ -285,3 +285,18 @@ def test_frame_split_footprint_and_graph(cornell_scene):
     got = pt.read_rgba32f()
     pt.close()
     assert_bitwise(got, want, "graph, split")
+
+
+def test_nan_rays(cornell_scene, V):
+    """A NaN camera position makes every camera ray NaN: it can never hit (the render
+    kernels skip its walk), while the counting build still walks and counts every node the
+    reference's walk visits (:393-431 with IEEE NaN compares)."""
+    sc = {k: np.array(v, copy=True) for k, v in cornell_scene.items()}
+    sc["cam"][0] = np.float32("nan")
+    want, want_cnt = O.render(sc, 32, 24, max_bounce=4, n_frames=2, counters=True)
+    got = gpu_render(sc, 32, 24, max_bounce=4, n_frames=2, variant=V)
+    assert_bitwise(got, want, "NaN origin")
+    got_img, (ms, cnt) = gpu_render(sc, 32, 24, max_bounce=4, n_frames=2, counting=True, variant=V)
+    assert_bitwise(got_img, want, "NaN origin, counting build")
+    assert [cnt["segments"], cnt["node_visits"], cnt["tri_tests"], cnt["sphere_tests"], cnt["hits"]] == \
+        [int(x) for x in want_cnt]
