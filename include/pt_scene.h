@@ -30,6 +30,17 @@ typedef struct pt_scene pt_scene;
  * Emission strength is forced to 7.5 for loaded materials (geometry_loader.h:84). */
 int pt_scene_load_obj(const char* obj_path, const char* mtl_path, pt_scene** out);
 
+/* Loader selection for pt_scene_load_obj_ex. */
+#define PT_LOAD_REFERENCE 0  /* exactly pt_scene_load_obj (the reference's parser semantics) */
+#define PT_LOAD_ROBUST 1     /* general Wavefront reader: f corners v, v/vt,
+                                v/vt/vn, v//vn, negative indices, polygons (fan-triangulated),
+                                comments, continuations, any line length, MTL properties in any
+                                order, `mtllib` when mtl_path is NULL; malformed input is a
+                                PT_E_PARSE with file:line.  Same material mapping as the
+                                reference (Kd, Ke, Ks, Ns/1000, strength 7.5), and the same
+                                arrays on files the reference reads correctly. */
+int pt_scene_load_obj_ex(const char* obj_path, const char* mtl_path, int flags, pt_scene** out);
+
 /* Wraps caller arrays (copied) in a scene object: n_tris*16 and n_mats*16 floats. */
 int pt_scene_from_arrays(const float* tris, int n_tris, const float* mats, int n_mats,
                          pt_scene** out);

@@ -21,9 +21,11 @@
 
 static void usage() {
     std::fprintf(stderr,
-                 "usage: ptrace <scene.obj> <scene.mtl> [--width W] [--height H] [--spp S] [--chunk C]\n"
+                 "usage: ptrace <scene.obj> <scene.mtl | -> [--width W] [--height H] [--spp S] [--chunk C]\n"
                  "              [--bounces B] [--mode 1..4] [--gpus G] [--pfm out.pfm] [--ppm out.ppm]\n"
-                 "              [--camera px py pz dx dy dz]\n");
+                 "              [--camera px py pz dx dy dz] [--robust]\n"
+                 "  --robust  general Wavefront ingest (v/vt/vn corners, polygons, negative indices,\n"
+                 "            free-form MTL; '-' as the MTL uses the OBJ's mtllib)\n");
 }
 
 #define CHECK(expr, ctx)                                                              \
@@ -42,6 +44,7 @@ int main(int argc, char** argv) {
     int W = 1000, H = 800, spp = 64, chunk = 16, bounces = 5, mode = 1, gpus = 1;   // ogl_path_trace.h:45-46
     std::string pfm = "out.pfm", ppm = "out.ppm";
     float cam[12] = {0, -6, 1, 0, 0, 1, 0, 0, 0, 0, 0, 0};                          // ogl_path_trace.h:53-54
+    bool robust = false;
     for (int i = 3; i < argc; i++) {
         std::string a = argv[i];
         auto next = [&](void) -> const char* { if (i + 1 >= argc) { usage(); std::exit(2); } return argv[++i]; };
@@ -55,13 +58,16 @@ int main(int argc, char** argv) {
         else if (a == "--pfm") pfm = next();
         else if (a == "--ppm") ppm = next();
         else if (a == "--camera") { for (int k = 0; k < 6; k++) cam[k < 3 ? k : k + 1] = (float)std::atof(next()); }
+        else if (a == "--robust") robust = true;
         else { usage(); return 2; }
     }
     if (spp < 1 || chunk < 1 || gpus < 1) { usage(); return 2; }
 
     auto t0 = std::chrono::steady_clock::now();
     pt_scene* sc = nullptr;
-    int rc = pt_scene_load_obj(obj, mtl, &sc);
+    const bool mtl_from_obj = std::string(mtl) == "-";
+    if (mtl_from_obj && !robust) { std::fprintf(stderr, "'-' as the MTL needs --robust\n"); return 2; }
+    int rc = pt_scene_load_obj_ex(obj, mtl_from_obj ? nullptr : mtl, robust ? PT_LOAD_ROBUST : PT_LOAD_REFERENCE, &sc);
     if (!rc) rc = pt_scene_add_builtins(sc);
     if (!rc) rc = pt_scene_build_bvh(sc);
     if (rc) { std::fprintf(stderr, "scene: %s (%d)\n", pt_scene_last_error(sc), rc); pt_scene_free(sc); return 1; }

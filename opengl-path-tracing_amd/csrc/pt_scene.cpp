@@ -231,6 +231,211 @@ int load_obj(const char* obj_path, const char* mtl_path, pt_scene& S) {
     return PT_OK;
 }
 
+// ---------------------------------------------------------------- robust ingest
+// A general Wavefront reader producing the same std140 records.  On files the reference
+// parser reads correctly (8-line MTL blocks, `v` / `f a b c` / `usemtl`) it yields the same
+// arrays bit for bit (tests/test_scene.py); beyond that it accepts what real exports
+// contain -- `f` corners as v, v/vt, v/vt/vn, v//vn, negative (relative) indices, polygons
+// (fan-triangulated v0,vi,vi+1), `vt`/`vn`/`vp`/`o`/`g`/`s`/`l`/`p`, comments, `\`
+// continuations, any line length, MTL properties in any order and number, `mtllib` -- and
+// reports malformed input with the file and line instead of istream's silent zeros.
+// Material mapping stays the reference's: Kd -> color, Ke -> emission, Ks -> specular,
+// Ns/1000 -> specular probability, smoothness 1 iff that is > 0, emission strength 7.5.
+struct Liner {
+    std::vector<std::string> lines;
+    std::vector<int> line_no;          // 1-based source line of each logical line
+    void build(const std::string& text) {
+        std::vector<std::pair<const char*, const char*>> L;
+        split_lines(text, L);
+        std::string acc;
+        int start = 0;
+        for (size_t i = 0; i < L.size(); i++) {
+            std::string ln(L[i].first, L[i].second);
+            if (!ln.empty() && ln.back() == '\r') ln.pop_back();
+            if (acc.empty()) start = (int)i + 1;
+            if (!ln.empty() && ln.back() == '\\') {      // continuation
+                ln.pop_back();
+                acc += ln;
+                acc += ' ';
+                continue;
+            }
+            acc += ln;
+            size_t h = acc.find('#');
+            if (h != std::string::npos) acc.resize(h);
+            lines.push_back(acc);
+            line_no.push_back(start);
+            acc.clear();
+        }
+        if (!acc.empty()) { lines.push_back(acc); line_no.push_back(start); }
+    }
+};
+
+void tokenize(const std::string& s, std::vector<std::string>& out) {
+    out.clear();
+    size_t i = 0, n = s.size();
+    while (i < n) {
+        while (i < n && Cursor::ws(s[i])) i++;
+        size_t j = i;
+        while (j < n && !Cursor::ws(s[j])) j++;
+        if (j > i) out.emplace_back(s, i, j - i);
+        i = j;
+    }
+}
+
+bool parse_f(const std::string& t, float& v) {
+    if (t.empty()) return false;
+    Cursor c{t.data(), t.data() + t.size()};
+    if (!c.num_f(v)) return false;
+    return c.p == c.e;                    // the whole token is one number
+}
+
+// One face corner "v", "v/vt", "v/vt/vn" or "v//vn" -> 0-based vertex index, or -1.
+long long corner_index(const std::string& t, long long nv) {
+    size_t slash = t.find('/');
+    std::string head = t.substr(0, slash);
+    if (head.empty()) return -1;
+    char* endp = nullptr;
+    errno = 0;
+    long long k = std::strtoll(head.c_str(), &endp, 10);
+    if (*endp != '\0' || errno == ERANGE || k == 0) return -1;
+    long long idx = k > 0 ? k - 1 : nv + k;     // negative: relative to the vertices so far
+    return (idx >= 0 && idx < nv) ? idx : -1;
+}
+
+std::string dir_of(const char* path) {
+    std::string p(path);
+    size_t s = p.find_last_of('/');
+    return s == std::string::npos ? std::string() : p.substr(0, s + 1);
+}
+
+int load_mtl_robust(const char* mtl_path, pt_scene& S, std::unordered_map<std::string, int>& mmap) {
+    std::string text;
+    if (!read_file(mtl_path, text)) { S.err = std::string("Failed to open material file: ") + mtl_path; return PT_E_IO; }
+    Liner L;
+    L.build(text);
+    std::vector<std::string> tk;
+    float col[4], emi[4], spc[4], dat[4];
+    bool open = false;
+    std::string name;
+    auto flush = [&]() {
+        if (!open) return;
+        if (dat[2] > 0) dat[1] = 1.0f;
+        dat[0] = 7.5f;
+        for (float* q : {col, emi, spc, dat}) S.mats.insert(S.mats.end(), q, q + 4);
+        mmap[name] = (int)(S.mats.size() / 16) - 1;
+        open = false;
+    };
+    for (size_t i = 0; i < L.lines.size(); i++) {
+        tokenize(L.lines[i], tk);
+        if (tk.empty()) continue;
+        auto bad = [&](const char* what) {
+            S.err = std::string(mtl_path) + ":" + std::to_string(L.line_no[i]) + ": " + what;
+            return PT_E_PARSE;
+        };
+        const std::string& key = tk[0];
+        if (key == "newmtl") {
+            flush();
+            if (tk.size() < 2) return bad("newmtl without a name");
+            name = tk[1];
+            for (float* q : {col, emi, spc, dat}) q[0] = q[1] = q[2] = q[3] = 0.0f;
+            open = true;
+        } else if (key == "Kd" || key == "Ks" || key == "Ke") {
+            if (!open) return bad("material property before newmtl");
+            if (tk.size() < 2) return bad("colour without components");
+            if (tk[1] == "spectral" || tk[1] == "xyz") return bad("only rgb colours are supported");
+            float v[3];
+            if (!parse_f(tk[1], v[0])) return bad("malformed number");
+            v[1] = v[2] = v[0];                          // "Kd r" means r r r
+            if (tk.size() >= 4) {
+                if (!parse_f(tk[2], v[1]) || !parse_f(tk[3], v[2])) return bad("malformed number");
+            } else if (tk.size() == 3) {
+                return bad("colour with two components");
+            }
+            float* dst = key == "Kd" ? col : key == "Ke" ? emi : spc;
+            dst[0] = v[0]; dst[1] = v[1]; dst[2] = v[2];
+        } else if (key == "Ns") {
+            if (!open) return bad("material property before newmtl");
+            float z;
+            if (tk.size() < 2 || !parse_f(tk[1], z)) return bad("malformed number");
+            dat[2] = (float)((double)z / 1000.0);
+        }
+        // Ka, Ni, d, Tr, Tf, illum, map_*, bump, ... carry nothing the shader reads
+    }
+    flush();
+    S.n_loaded_mats = (int)(S.mats.size() / 16);
+    return PT_OK;
+}
+
+int load_obj_robust(const char* obj_path, const char* mtl_path, pt_scene& S) {
+    std::string otext;
+    if (!read_file(obj_path, otext)) { S.err = std::string("Failed to open vertex file: ") + obj_path; return PT_E_IO; }
+    Liner L;
+    L.build(otext);
+    std::unordered_map<std::string, int> mmap;
+    std::vector<std::string> tk;
+    // MTL: the given file, else the OBJ's first `mtllib` (relative to the OBJ's directory)
+    std::string mtl = mtl_path ? std::string(mtl_path) : std::string();
+    if (mtl.empty()) {
+        for (auto& ln : L.lines) {
+            tokenize(ln, tk);
+            if (tk.size() >= 2 && tk[0] == "mtllib") {
+                std::string rest = ln.substr(ln.find("mtllib") + 6);
+                size_t a = rest.find_first_not_of(" \t"), b = rest.find_last_not_of(" \t\r");
+                mtl = dir_of(obj_path) + rest.substr(a, b - a + 1);
+                break;
+            }
+        }
+    }
+    if (!mtl.empty()) {
+        int rc = load_mtl_robust(mtl.c_str(), S, mmap);
+        if (rc) return rc;
+    }
+    std::vector<float> verts;
+    std::vector<long long> poly;
+    std::string cur;
+    for (size_t i = 0; i < L.lines.size(); i++) {
+        tokenize(L.lines[i], tk);
+        if (tk.empty()) continue;
+        auto bad = [&](const std::string& what) {
+            S.err = std::string(obj_path) + ":" + std::to_string(L.line_no[i]) + ": " + what;
+            return PT_E_PARSE;
+        };
+        const std::string& key = tk[0];
+        if (key == "v") {
+            float v[3];
+            if (tk.size() < 4) return bad("vertex with fewer than 3 coordinates");
+            for (int q = 0; q < 3; q++)
+                if (!parse_f(tk[1 + q], v[q])) return bad("malformed number");
+            verts.insert(verts.end(), {v[0], v[1], v[2]});
+        } else if (key == "f") {
+            const long long nv = (long long)(verts.size() / 3);
+            poly.clear();
+            for (size_t q = 1; q < tk.size(); q++) {
+                long long idx = corner_index(tk[q], nv);
+                if (idx < 0) return bad("face corner '" + tk[q] + "' is not a valid vertex reference");
+                poly.push_back(idx);
+            }
+            if (poly.size() < 3) return bad("face with fewer than 3 corners");
+            auto it = mmap.find(cur);
+            int midx = 0;
+            if (it == mmap.end()) mmap.emplace(cur, 0);   // as the reference: unknown -> 0
+            else midx = it->second;
+            for (size_t q = 1; q + 1 < poly.size(); q++) {
+                for (long long c : {poly[0], poly[q], poly[q + 1]}) {
+                    const float* v = &verts[3 * c];
+                    S.tris.insert(S.tris.end(), {v[0], v[1], v[2], 0.0f});
+                }
+                S.tris.insert(S.tris.end(), {(float)midx, 0.0f, 0.0f, 0.0f});
+            }
+        } else if (key == "usemtl") {
+            if (tk.size() < 2) return bad("usemtl without a name");
+            cur = tk[1];
+        }
+        // vt, vn, vp, o, g, s, l, p, mtllib, ... carry nothing the shader reads
+    }
+    return PT_OK;
+}
+
 // ---------------------------------------------------------------- BVH
 struct Box { float mn[3], mx[3]; };
 inline Box empty_box() {
@@ -429,6 +634,18 @@ int pt_scene_load_obj(const char* obj_path, const char* mtl_path, pt_scene** out
     pt_scene* s = new pt_scene();
     int rc = load_obj(obj_path, mtl_path, *s);
     *out = s;   // returned even on error so pt_scene_last_error() can explain
+    return rc;
+}
+
+int pt_scene_load_obj_ex(const char* obj_path, const char* mtl_path, int flags, pt_scene** out) {
+    if (!out) return PT_E_ARG;
+    *out = nullptr;
+    if (!obj_path) return PT_E_ARG;
+    if (flags & ~PT_LOAD_ROBUST) return PT_E_ARG;
+    if (!(flags & PT_LOAD_ROBUST)) return pt_scene_load_obj(obj_path, mtl_path, out);
+    pt_scene* s = new pt_scene();
+    int rc = load_obj_robust(obj_path, mtl_path, *s);
+    *out = s;
     return rc;
 }
 

@@ -64,6 +64,7 @@ def lib():
         vp, ip, fp = C.c_void_p, C.c_int, C.c_float
         sig = {
             "pt_scene_load_obj": (ip, [C.c_char_p, C.c_char_p, C.POINTER(vp)]),
+            "pt_scene_load_obj_ex": (ip, [C.c_char_p, C.c_char_p, ip, C.POINTER(vp)]),
             "pt_scene_from_arrays": (ip, [_F, ip, _F, ip, C.POINTER(vp)]),
             "pt_scene_add_builtins": (ip, [vp]),
             "pt_scene_build_bvh": (ip, [vp]),
@@ -162,6 +163,20 @@ def load_vertex_data(obj_path, mtl_path):
     """geometry_loader.h:15 -> (tris[N,16], mats[M,16]) float32 std140 records."""
     h = C.c_void_p()
     rc = lib().pt_scene_load_obj(str(obj_path).encode(), str(mtl_path).encode(), C.byref(h))
+    s = _Scene(h)
+    s.check(rc)
+    a = s.arrays()
+    return a["tris"], a["mats"]
+
+
+def load_obj_robust(obj_path, mtl_path=None):
+    """General Wavefront ingest (pt_scene_load_obj_ex, PT_LOAD_ROBUST) -> (tris, mats);
+    mtl_path None = the OBJ's `mtllib`."""
+    h = C.c_void_p()
+    rc = lib().pt_scene_load_obj_ex(str(obj_path).encode(), None if mtl_path is None else str(mtl_path).encode(),
+                                    1, C.byref(h))
+    if not h.value:
+        raise PTError(rc, "pt_scene_load_obj_ex failed")
     s = _Scene(h)
     s.check(rc)
     a = s.arrays()
