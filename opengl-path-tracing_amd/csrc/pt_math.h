@@ -45,6 +45,40 @@ PT_HD float fsqrt(float x) {
 #endif
 }
 
+// Guarded fast forms of the correctly rounded reciprocal and square root, for arguments the
+// caller has bounded to [2^-100, 2^100] in magnitude (no scaling, no special cases): one
+// v_rcp_f32 / v_sqrt_f32 plus fma corrections.  Bit-identical to 1.0f/x and sqrtf(x) over
+// EVERY binary32 in that range on gfx950 -- checked exhaustively by tools/verify_fastmath.hip
+// (tests/test_gpu_fastmath.py).  Host builds use the IEEE operations themselves.
+PT_HD float rcp_fast(float x) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    float y = __builtin_amdgcn_rcpf(x);
+    float e = __builtin_fmaf(-x, y, 1.0f);
+    return __builtin_fmaf(e, y, y);
+#else
+    return 1.0f / x;
+#endif
+}
+PT_HD float sqrt_fast(float x) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    float s = __builtin_amdgcn_sqrtf(x);
+    float sd = __uint_as_float(__float_as_uint(s) - 1u), su = __uint_as_float(__float_as_uint(s) + 1u);
+    float rd = __builtin_fmaf(-sd, s, x), ru = __builtin_fmaf(-su, s, x);
+    s = rd <= 0.0f ? sd : s;
+    return ru > 0.0f ? su : s;
+#else
+    return sqrtf(x);
+#endif
+}
+
+// a / b for |a| in [2^-20, 2^60] and b with RN(1/b) = rb exactly (Markstein: the remainder
+// a - q0*b is exact and fma(r, rb, q0) is the correctly rounded quotient).
+PT_HD float div_mk(float a, float b, float rb) {
+    float q = a * rb;
+    float r = __builtin_fmaf(-q, b, a);
+    return __builtin_fmaf(r, rb, q);
+}
+
 // fdlibm e_logf (FreeBSD constants).  x in {0} U [2^-32, 1] on the hot path.
 PT_HD float logf_pinned(float x) {
     const float ln2_hi = 6.9313812256e-01f, ln2_lo = 9.0580006145e-06f, two25 = 3.355443200e+07f;
@@ -76,7 +110,10 @@ PT_HD float logf_pinned(float x) {
         dk = (float)k;
         return dk * ln2_hi - ((R - dk * ln2_lo) - f);
     }
-    float s = f / (2.0f + f);
+    // |f| >= 2^-20 on this path (the branch above takes smaller f) and 2+f in [1.58, 2.42]:
+    // the quotient by an exact reciprocal (rcp_fast) and a Markstein correction
+    const float tf = 2.0f + f;
+    float s = div_mk(f, tf, rcp_fast(tf));
     dk = (float)k;
     float z = s * s;
     int32_t ii = ix - (0x6147a << 3);
@@ -131,8 +168,21 @@ PT_HD f3 operator*(f3 a, float s) { return mk(a.x * s, a.y * s, a.z * s); }
 PT_HD f3 operator/(f3 a, float s) { return mk(a.x / s, a.y / s, a.z / s); }
 PT_HD float dot(f3 a, f3 b) { return (a.x * b.x + a.y * b.y) + a.z * b.z; }
 PT_HD f3 cross(f3 a, f3 b) { return mk(a.y * b.z - b.y * a.z, a.z * b.x - b.z * a.x, a.x * b.y - b.x * a.y); }
-PT_HD float length(f3 a) { return fsqrt(dot(a, a)); }
-PT_HD f3 normalize(f3 a) { float r = 1.0f / fsqrt(dot(a, a)); return a * r; }
+// The guard of rcp_fast / sqrt_fast; NaN fails it.
+PT_HD bool fast_range(float q) { return q >= 0x1p-100f && q <= 0x1p100f; }
+PT_HD float sqrt_g(float q) {
+    if (fast_range(q)) return sqrt_fast(q);
+    return fsqrt(q);
+}
+PT_HD float length(f3 a) { return sqrt_g(dot(a, a)); }
+// v * (1/sqrt(dot(v,v))): the two correctly rounded steps, each by its guarded fast form
+// (dot in [2^-100, 2^100] puts the root in [2^-50, 2^50]).
+PT_HD f3 normalize(f3 a) {
+    float q = dot(a, a), r;
+    if (fast_range(q)) r = rcp_fast(sqrt_fast(q));
+    else r = 1.0f / fsqrt(q);
+    return a * r;
+}
 PT_HD f3 mix(f3 x, f3 y, float a) {
     float oma = 1.0f - a;
     return mk(x.x * oma + y.x * a, x.y * oma + y.y * a, x.z * oma + y.z * a);
@@ -147,7 +197,7 @@ PT_HD uint32_t next_random(uint32_t& s) {
 PT_HD float random01(uint32_t& s) { return (float)next_random(s) * (1.0f / 4294967296.0f); }
 PT_HD float random_normal(uint32_t& s) {            // :115-120 (theta first, then rho)
     float theta = (2.0f * 3.1415926f) * random01(s);
-    float rho = fsqrt(-2.0f * logf_pinned(random01(s)));
+    float rho = sqrt_g(-2.0f * logf_pinned(random01(s)));
     return rho * cosf_pinned(theta);
 }
 PT_HD f3 random_unit_vector(uint32_t& s) {          // :122-129, x, y, z order

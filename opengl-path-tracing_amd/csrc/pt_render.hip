@@ -65,6 +65,7 @@ struct KParams {
     // group = n_frames and rgb = null: the lane owns all frames and accumulates in registers.
     int group;
     float4* rgb;
+    float rW, rH;                  // RN(1/W), RN(1/H) (host IEEE division) for the camera ray
 };
 
 // Progressive mode (hipGraph replay): the frame range comes from a device counter, and
@@ -1029,8 +1030,11 @@ __global__ __launch_bounds__(256, MINW) void k_render_sm(KParams p) {
                         ax = pt::random01(state);
                         ay = pt::random01(state);
                     }
-                    float u = ((float)lx + ax) / (float)p.W - 0.5f;
-                    float v = ((float)y + ay) / (float)p.H - 0.5f;
+                    // (x + jitter) / W by the exact reciprocal RN(1/W) and a Markstein
+                    // correction: the numerator is 0 or in [2^-32, 2^17), W <= 2^16, so the
+                    // remainder is exact and the quotient correctly rounded (test_exact_div)
+                    float u = pt::div_mk((float)lx + ax, (float)p.W, p.rW) - 0.5f;
+                    float v = pt::div_mk((float)y + ay, (float)p.H, p.rH) - 0.5f;
                     d = pt::normalize((cfwd + cright * u) + cup * v);
                     o = cpos;
                     inc = mk(0, 0, 0);
@@ -1042,7 +1046,8 @@ __global__ __launch_bounds__(256, MINW) void k_render_sm(KParams p) {
                 fast = p.scene_fast && in_guard(o.x, 0x1p-40f, 0x1p60f) && in_guard(o.y, 0x1p-40f, 0x1p60f) &&
                        in_guard(o.z, 0x1p-40f, 0x1p60f) && in_guard(d.x, 0x1p-20f, 2.0f) && d.x != 0.0f &&
                        in_guard(d.y, 0x1p-20f, 2.0f) && d.y != 0.0f && in_guard(d.z, 0x1p-20f, 2.0f) && d.z != 0.0f;
-                if (fast) rd = mk(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
+                // under the guard |d_i| is in [2^-20, 2]: rcp_fast is the exact RN(1/d_i)
+                if (fast) rd = mk(pt::rcp_fast(d.x), pt::rcp_fast(d.y), pt::rcp_fast(d.z));
                 if (COUNT && !fast) c.slow++;
                 if (COUNT && ray_has_nan(o, d)) c.nan++;
                 t = __builtin_huge_valf();
@@ -1541,6 +1546,8 @@ static int enqueue_render(pt_ctx* c, int frame_first, int n_frames, int acc_firs
         p.leaf_thresh = c->leaf_thresh ? c->leaf_thresh : (lds_scene ? 32 : 16);
         p.shade_thresh = c->shade_thresh ? c->shade_thresh : (lds_scene ? 48 : 32);
     }
+    p.rW = 1.0f / (float)p.W;
+    p.rH = 1.0f / (float)p.H;
     p.group = plan_group(c, n_frames);
     if (p.group < n_frames) {
         int rc = ensure_rgb(c, n_frames);

@@ -47,6 +47,50 @@ int main(int argc, char** argv) {
 """
 
 
+PROG_CAM = r"""
+#include <math.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+static uint64_t s = 0x2545F4914F6CDD1Dull;
+static uint64_t rnd(void) { s ^= s << 13; s ^= s >> 7; s ^= s << 17; return s; }
+static uint32_t fb(float f) { uint32_t u; memcpy(&u, &f, 4); return u; }
+int main(void) {
+    long long bad = 0, n = 0;
+    for (int W = 1; W <= 65536; W++) {
+        float w = (float)W, rw = 1.0f / w;
+        for (int k = 0; k < 400; k++) {
+            uint64_t r = rnd();
+            int x = (int)(r % (uint64_t)(W + 1));
+            float j = (float)(uint32_t)(r >> 32) * (1.0f / 4294967296.0f);   /* random() in [0,1] */
+            if (k == 0) j = 0.0f;
+            if (k == 1) j = 1.0f;
+            float a = (float)x + j;
+            float q0 = a * rw, rem = fmaf(-q0, w, a), q = fmaf(rem, rw, q0), ex = a / w;
+            n++;
+            if (fb(q) != fb(ex)) { if (bad < 5) printf("a=%a W=%d got %a want %a\n", a, W, q, ex); bad++; }
+        }
+    }
+    printf("n=%lld bad=%lld\n", n, bad);
+    return bad != 0;
+}
+"""
+
+
+def test_camera_quotient_is_correctly_rounded(tmp_path):
+    """The kernel's camera ray divides (x + jitter) by W with RN(1/W) and a Markstein
+    correction (pt_render.hip): every W in [1, 2^16] with 400 numerators each, including
+    jitter 0 and 1, against IEEE division."""
+    src = tmp_path / "cam.c"
+    src.write_text(PROG_CAM)
+    exe = tmp_path / "cam"
+    subprocess.check_call(["gcc", "-O2", "-ffp-contract=off", "-march=x86-64-v3", str(src), "-o", str(exe), "-lm"])
+    out = subprocess.run([str(exe)], capture_output=True, text=True)
+    assert out.returncode == 0, out.stdout
+    assert "bad=0" in out.stdout
+
+
 def test_markstein_quotient_is_correctly_rounded(tmp_path):
     src = tmp_path / "mk.c"
     src.write_text(PROG)
