@@ -1482,9 +1482,11 @@ int pt_set_tuning(pt_ctx* c, int key, int value) {
 // Measured (C2 scene, 64-frame launches): 8 frames per item +6% over whole-pixel items on
 // one GPU, 2-4 frames +85% on a 1080p/8 share; so ~16 items per resident lane, capped at
 // 8 frames.  group == n_frames is the register mode (a lane owns all frames of a pixel and
-// accumulates in registers); the counting build always uses it.
+// accumulates in registers).  The counting build follows the same plan: with whole-pixel
+// items a 1080p/8 share of a 1024-frame launch would run each lane through 1024 frames
+// in sequence (minutes).
 static int plan_group(const pt_ctx* c, int n_frames) {
-    if ((c->variant != 0 && c->variant != 3) || c->counting) return n_frames;
+    if (c->variant != 0 && c->variant != 3) return n_frames;
     if (c->group_force > 0) return std::min(c->group_force, n_frames);
     const int waves = c->minw ? c->minw : 6;
     const double lanes = (double)c->n_cu * 4.0 * waves * 64.0;
@@ -1597,7 +1599,8 @@ static int enqueue_render(pt_ctx* c, int frame_first, int n_frames, int acc_firs
         // a tie for global-memory scenes
         const int mw = c->minw ? c->minw : 6;
 #define PT_LAUNCH_SM(L, M)                                                                                    \
-    if (c->counting) hipLaunchKernelGGL((k_render_sm<true, L, 5, M, false>), grid, dim3(256), L ? lds : 0, c->stream, p); \
+    if (c->counting && p.rgb) hipLaunchKernelGGL((k_render_sm<true, L, 5, M, true>), grid, dim3(256), L ? lds : 0, c->stream, p); \
+    else if (c->counting) hipLaunchKernelGGL((k_render_sm<true, L, 5, M, false>), grid, dim3(256), L ? lds : 0, c->stream, p); \
     else if (p.rgb && mw == 6) hipLaunchKernelGGL((k_render_sm<false, L, 6, M, true>), grid, dim3(256), L ? lds : 0, c->stream, p); \
     else if (p.rgb) hipLaunchKernelGGL((k_render_sm<false, L, 5, M, true>), grid, dim3(256), L ? lds : 0, c->stream, p); \
     else if (mw == 6) hipLaunchKernelGGL((k_render_sm<false, L, 6, M, false>), grid, dim3(256), L ? lds : 0, c->stream, p); \

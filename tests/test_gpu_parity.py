@@ -300,3 +300,21 @@ def test_nan_rays(cornell_scene, V):
     assert_bitwise(got_img, want, "NaN origin, counting build")
     assert [cnt["segments"], cnt["node_visits"], cnt["tri_tests"], cnt["sphere_tests"], cnt["hits"]] == \
         [int(x) for x in want_cnt]
+
+
+@pytest.mark.parametrize("group", [1, 3, 64])
+def test_counters_every_work_item_size(cornell_scene, group):
+    """The counting build with frame-split items and with whole-pixel items (register mode)
+    reports the oracle's reference-semantics counts and the same image."""
+    want_img, want_cnt = O.render(cornell_scene, 40, 36, max_bounce=8, n_frames=6, counters=True)
+    pt = H.PathTracer(40, 36, max_bounce=8)
+    pt.set_tuning(group=group)
+    pt.upload(cornell_scene)
+    pt.set_counting(True)
+    pt.render(1, 6, 0)
+    img = pt.read_rgba32f()
+    ms, cnt = pt.stats()
+    pt.close()
+    assert_bitwise(img, want_img, "counting, group %d" % group)
+    assert [cnt["segments"], cnt["node_visits"], cnt["tri_tests"], cnt["sphere_tests"], cnt["hits"]] == \
+        [int(x) for x in want_cnt]
