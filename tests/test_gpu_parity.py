@@ -318,3 +318,46 @@ def test_counters_every_work_item_size(cornell_scene, group):
     assert_bitwise(img, want_img, "counting, group %d" % group)
     assert [cnt["segments"], cnt["node_visits"], cnt["tri_tests"], cnt["sphere_tests"], cnt["hits"]] == \
         [int(x) for x in want_cnt]
+
+
+def _tri(v0, v1, v2, m=0):
+    t = np.zeros(16, np.float32)
+    t[0:3], t[4:7], t[8:11], t[12] = v0, v1, v2, m
+    return t
+
+
+def test_edge_scenes(cornell_scene, V):
+    """Scenes at the edges of the input space: no triangles (sphere only), one triangle (a
+    single-triangle leaf, tri0 == tri1), and two coincident triangles (exact ties in the
+    leaf's 2-way choice, :411-428)."""
+    mats = cornell_scene["mats"][: cornell_scene["n_loaded_mats"]]
+    one = _tri((-2, 2, 0), (2, 2, 0), (0, 2, 3), 1)[None]
+    twin = np.stack([_tri((-2, 3, -1), (2, 3, -1), (0, 3, 4), 2), _tri((-2, 3, -1), (2, 3, -1), (0, 3, 4), 3)])
+    for tris in (np.zeros((0, 16), np.float32), one, twin):
+        sc = H.scene_from_arrays(tris, mats)
+        want = O.render(sc, 24, 20, max_bounce=6, n_frames=3)
+        got = gpu_render(sc, 24, 20, max_bounce=6, n_frames=3, variant=V)
+        assert_bitwise(got, want, "%d triangles" % len(tris))
+
+
+@pytest.mark.parametrize("W,Hh", [(1, 1), (1, 9), (13, 1), (9, 7)])
+def test_tiny_and_ragged_images(cornell_scene, W, Hh, V):
+    """Images smaller than one 8x8 tile and ragged tile edges."""
+    want = O.render(cornell_scene, W, Hh, max_bounce=8, n_frames=4)
+    got = gpu_render(cornell_scene, W, Hh, max_bounce=8, n_frames=4, variant=V)
+    assert_bitwise(got, want, "%dx%d" % (W, Hh))
+
+
+def test_zero_bounces_and_huge_frame_numbers(cornell_scene, V):
+    """maxBounceCount = 0 (one segment per path) and frame numbers near 2^24 and 2^31, where
+    float(frame) in the running mean rounds and the seed term wraps (:514-515, :548-551)."""
+    want = O.render(cornell_scene, 20, 16, max_bounce=0, n_frames=2)
+    got = gpu_render(cornell_scene, 20, 16, max_bounce=0, n_frames=2, variant=V)
+    assert_bitwise(got, want, "0 bounces")
+    prior = np.random.default_rng(5).random((16, 20, 4), dtype=np.float32)
+    for f0 in ((1 << 24) - 1, (1 << 31) - 3):
+        want = O.render(cornell_scene, 20, 16, max_bounce=3, frame_first=f0, n_frames=3, acc_first=1,
+                        accum=prior.copy())
+        got = gpu_render(cornell_scene, 20, 16, max_bounce=3, frame_first=f0, n_frames=3, acc_first=1,
+                         prior=prior, variant=V)
+        assert_bitwise(got, want, "frame %d" % f0)
