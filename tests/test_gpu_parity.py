@@ -361,3 +361,29 @@ def test_zero_bounces_and_huge_frame_numbers(cornell_scene, V):
         got = gpu_render(cornell_scene, 20, 16, max_bounce=3, frame_first=f0, n_frames=3, acc_first=1,
                          prior=prior, variant=V)
         assert_bitwise(got, want, "frame %d" % f0)
+
+
+def test_c1_config_counts_and_image(cornell_scene):
+    """SURVEY.md §8(d) C1 in full: Cornell 256x256, 1 spp, maxBounceCount 4, the reference's
+    glDispatchCompute(W/10, H/10) footprint -- image and reference-semantics counts equal the
+    oracle's."""
+    want, want_cnt = O.render(cornell_scene, 256, 256, max_bounce=4, n_frames=1, counters=True)
+    got, (ms, cnt) = gpu_render(cornell_scene, 256, 256, max_bounce=4, n_frames=1,
+                                flags=H.PT_FLAG_REF_DISPATCH, counting=True)
+    assert_bitwise(got[:250, :250], want[:250, :250], "C1 footprint")
+    assert np.all(got[250:] == 0) and np.all(got[:, 250:] == 0)
+    # the oracle rendered every pixel; count the footprint's share with render_pixels
+    ys, xs = np.mgrid[0:250, 0:250]
+    _, fp_cnt = O.render_pixels(cornell_scene, 256, 256, xs.ravel(), ys.ravel(), max_bounce=4, n_frames=1,
+                                counters=True)
+    assert [cnt["segments"], cnt["node_visits"], cnt["tri_tests"], cnt["sphere_tests"], cnt["hits"]] == \
+        [int(x) for x in fp_cnt]
+
+
+def test_c3_stand_in_reduced_spp_counts(big_scene):
+    """Reduced-spp C2/C3-style counts on a large scene (global-memory walk, frame-split items)."""
+    want, want_cnt = O.render(big_scene, 40, 24, max_bounce=8, n_frames=3, counters=True)
+    got, (ms, cnt) = gpu_render(big_scene, 40, 24, max_bounce=8, n_frames=3, counting=True)
+    assert_bitwise(got, want, "large scene, counting")
+    assert [cnt["segments"], cnt["node_visits"], cnt["tri_tests"], cnt["sphere_tests"], cnt["hits"]] == \
+        [int(x) for x in want_cnt]
