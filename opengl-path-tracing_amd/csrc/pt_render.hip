@@ -769,6 +769,7 @@ __global__ __launch_bounds__(256, MINW) void k_render_wave(KParams p) {
 // =====================================================================================
 enum : int { ST_DONE = 0, ST_TRAV = 1, ST_LEAF = 2, ST_SHADE = 3 };
 constexpr unsigned kPullBatch = 32;
+constexpr int kWalkUnroll = 4;   // node steps per yield check of the walk (measured: 1 -> 2 +3.6%, 4 +5.7%, 6/8 slower)
 
 // The TRAV phase: each TRAV lane advances one node per iteration (bvh_intersect + the link
 // choice of calculateRayCollision :389-431) until it stops at a leaf whose box it hit
@@ -785,7 +786,7 @@ __device__ __forceinline__ void trav_walk(const SceneView& S, f3 o, f3 d, f3 rd,
                                           unsigned long long live, int leaf_thresh, int shade_thresh,
                                           int& st, int& bi, int& leaf, Cnt& c) {
     const int min_thresh = leaf_thresh < shade_thresh ? leaf_thresh : shade_thresh;
-    for (;;) {
+    auto step = [&]() {
         if (st == ST_TRAV) {
             float4 lo, hi;
             node_at<LDS>(S, bi, lo, hi);
@@ -797,6 +798,10 @@ __device__ __forceinline__ void trav_walk(const SceneView& S, f3 o, f3 d, f3 rd,
             leaf = a;
             st = to_leaf ? ST_LEAF : (bi < 0 ? ST_SHADE : ST_TRAV);
         }
+    };
+    for (;;) {
+#pragma unroll
+        for (int u = 0; u < kWalkUnroll; u++) step();
         unsigned long long mt = __ballot(st == ST_TRAV);
         if (!mt) break;
         if (__popcll(live & ~mt) >= min_thresh) {
