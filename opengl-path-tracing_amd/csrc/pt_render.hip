@@ -371,9 +371,10 @@ struct SceneView {
 // planes -- node half h of node i at [h*np + i], triangle quad k of slot s at [k*tp + s] --
 // so random per-lane gathers of one half/quad hit 16-B bank groups spread over all 64
 // banks instead of every 2nd (nodes, 32-B stride) or 4th (triangles, 64-B stride) group.
+extern __shared__ float4 g_lds[];   // the state-machine kernel's scene copy (nodes first)
 template <bool LDS>
 __device__ __forceinline__ void node_at(const SceneView& S, int i, float4& lo, float4& hi) {
-    if (LDS) { lo = S.nodes[i]; hi = S.nodes[i + S.np]; }
+    if (LDS) { lo = g_lds[i]; hi = g_lds[i + S.np]; }   // LDS base 0: no address add
     else { lo = S.nodes[2 * i]; hi = S.nodes[2 * i + 1]; }
 }
 template <bool LDS>
@@ -793,10 +794,10 @@ __device__ __forceinline__ void trav_walk(const SceneView& S, f3 o, f3 d, f3 rd,
             int a = __float_as_int(hi.z), b = __float_as_int(hi.w);
             bool hb = (ALL_FAST || fast) ? slab_fast(lo, hi, o, d, rd, t) : slab(lo, hi, o, d, t);
             if (COUNT) { c.nodes++; diag_tick(c.tw, c.tl); }
-            const bool to_leaf = hb && a < 0;
-            bi = (hb && a >= 0) ? a : b;
+            const bool internal = a >= 0;      // one compare feeds both selects
+            bi = (hb && internal) ? a : b;
             leaf = a;
-            st = to_leaf ? ST_LEAF : (bi < 0 ? ST_SHADE : ST_TRAV);
+            st = (hb && !internal) ? ST_LEAF : (bi < 0 ? ST_SHADE : ST_TRAV);
         }
     };
     for (;;) {
