@@ -58,13 +58,12 @@ struct KParams {
     const unsigned* tile_perm;     // queue order of 8x8 tiles (null = raster order)
     unsigned* tile_cost;           // per-tile segment counts of this launch (null = off)
     // frame-split work items (state-machine kernel): a queue item is (pixel, `group`
-    // consecutive frames); with rgb != null the lane stores each frame's pixel colour to
-    // rgb[k * pixels + pixel] (frame planes: the accumulate pass reads coalesced, and the
-    // 8 lanes on one tile row write one 128-B line) and k_accum_frames applies the running
-    // mean in frame order.
+    // consecutive frames); with rgb != null the lane stores each frame's pixel colour (12 B)
+    // to rgb[3 * (k * pixels + pixel)] (frame planes: the accumulate pass reads coalesced)
+    // and k_accum_frames applies the running mean in frame order.
     // group = n_frames and rgb = null: the lane owns all frames and accumulates in registers.
     int group;
-    float4* rgb;
+    float* rgb;                    // 3 floats per (frame, pixel)
     float rW, rH;                  // RN(1/W), RN(1/H) (host IEEE division) for the camera ray
 };
 
@@ -290,13 +289,13 @@ __device__ __forceinline__ float4 accumulate(float4 prev, f3 rgb, int frame, boo
 }
 
 // Non-temporal 16-B accesses (streamed data that must not evict the scene from L2/MALL).
-typedef float nt_f4 __attribute__((ext_vector_type(4)));
-__device__ __forceinline__ void nt_store(float4* dst, float4 v) {
-    __builtin_nontemporal_store(nt_f4{v.x, v.y, v.z, v.w}, reinterpret_cast<nt_f4*>(dst));
+__device__ __forceinline__ void nt_store3(float* dst, f3 v) {
+    __builtin_nontemporal_store(v.x, dst);
+    __builtin_nontemporal_store(v.y, dst + 1);
+    __builtin_nontemporal_store(v.z, dst + 2);
 }
-__device__ __forceinline__ float4 nt_load(const float4* src) {
-    nt_f4 v = __builtin_nontemporal_load(reinterpret_cast<const nt_f4*>(src));
-    return make_float4(v.x, v.y, v.z, v.w);
+__device__ __forceinline__ f3 nt_load3(const float* src) {
+    return mk(__builtin_nontemporal_load(src), __builtin_nontemporal_load(src + 1), __builtin_nontemporal_load(src + 2));
 }
 
 __device__ __forceinline__ unsigned long long wave_sum(unsigned long long v) {
@@ -954,8 +953,7 @@ __global__ __launch_bounds__(256, MINW) void k_render_sm(KParams p) {
                         if (SPLIT) {
                             // streamed once, read once by k_accum_frames: non-temporal, so the
                             // colour stream does not evict the scene from L2/MALL
-                            nt_store(p.rgb + (size_t)k * (size_t)(p.rows_local * p.W) + (size_t)aidx,
-                                     make_float4(px.x, px.y, px.z, 0.0f));
+                            nt_store3(p.rgb + 3 * ((size_t)k * (size_t)(p.rows_local * p.W) + (size_t)aidx), px);
                         } else {
                             int f = p.frame_first + k;
                             acc = accumulate(acc, px, f, k > 0 || p.acc_first == 1);
@@ -1124,10 +1122,10 @@ __global__ __launch_bounds__(256) void k_accum_frames(KParams p) {
     const int crow = (int)(idx / p.W), cx = (int)(idx - (long long)crow * p.W);
     if (cx >= p.x_limit || p.row0 + crow * p.row_stride >= p.y_limit) return;
     float4 acc = p.acc_first ? p.accum[idx] : make_float4(0, 0, 0, 0);
-    const float4* src = p.rgb + idx;
+    const float* src = p.rgb + 3 * idx;
     for (int k = 0; k < p.n_frames; k++) {
-        float4 v = nt_load(src + (size_t)k * (size_t)n);
-        acc = accumulate(acc, mk(v.x, v.y, v.z), p.frame_first + k, k > 0 || p.acc_first == 1);
+        const f3 v = nt_load3(src + 3 * (size_t)k * (size_t)n);
+        acc = accumulate(acc, v, p.frame_first + k, k > 0 || p.acc_first == 1);
     }
     p.accum[idx] = acc;
 }
@@ -1187,7 +1185,7 @@ struct pt_ctx {
     // frame-split work items (KParams::group): 0 = automatic, n = frames per item
     int group_force = 0;
     int n_cu = 0;
-    float4* d_rgb = nullptr;       // per-(pixel, frame) colours of the frame-split mode
+    float* d_rgb = nullptr;        // per-(frame, pixel) colours of the frame-split mode
     size_t rgb_bytes = 0;
     bool scene_ok = false, cam_ok = false, counting = false;
     float cam[12] = {0};
@@ -1504,7 +1502,7 @@ static int plan_group(const pt_ctx* c, int n_frames) {
 }
 
 static int ensure_rgb(pt_ctx* c, int n_frames) {
-    size_t need = (size_t)std::max(c->rows_local, 1) * (size_t)c->cfg.width * (size_t)n_frames * sizeof(float4);
+    size_t need = (size_t)std::max(c->rows_local, 1) * (size_t)c->cfg.width * (size_t)n_frames * 3 * sizeof(float);
     if (need <= c->rgb_bytes) return PT_OK;
     (void)hipFree(c->d_rgb);
     c->d_rgb = nullptr;
