@@ -1485,7 +1485,7 @@ int pt_set_tuning(pt_ctx* c, int key, int value) {
 // colours go to a buffer and k_accum_frames applies the running mean in frame order.
 // Measured (C2 scene, 64-frame launches): 8 frames per item +6% over whole-pixel items on
 // one GPU, 2-4 frames +85% on a 1080p/8 share; so ~16 items per resident lane, capped at
-// 8 frames.  group == n_frames is the register mode (a lane owns all frames of a pixel and
+// 16 frames (4 for global-memory scenes).  group == n_frames is the register mode (a lane owns all frames of a pixel and
 // accumulates in registers).  The counting build follows the same plan: with whole-pixel
 // items a 1080p/8 share of a 1024-frame launch would run each lane through 1024 frames
 // in sequence (minutes).
@@ -1497,7 +1497,7 @@ static int plan_group(const pt_ctx* c, int n_frames) {
     const double px = (double)c->rows_local * c->cfg.width;
     const bool lds_scene = c->lds_bytes <= kLdsSceneMax && c->variant != 3;
     int g = (int)(px * n_frames / (16.0 * lanes));
-    g = std::max(1, std::min(g, lds_scene ? 8 : 4));   // C3 stand-in: 4 frames +8% over 8
+    g = std::max(1, std::min(g, lds_scene ? 16 : 4));  // C2: 16 +0.5% over 8; C3 stand-in: 4 +8% over 8
     return std::min(g, n_frames);
 }
 
