@@ -37,6 +37,12 @@ extern "C" {
 #define PT_FLAG_NO_TRIANGLES 8   /* render_triangles = false */
 #define PT_FLAG_REF_DISPATCH 16  /* write only the 10x10-group footprint of
                                     glDispatchCompute(W/10, H/10) (ogl_path_trace.h:183) */
+#define PT_FLAG_MOLLER_TRUMBORE 32 /* opt-in fast mode: the reference's (dead) Moller-Trumbore
+                                    RayIntersectsTriangle (computeShader.c:228-272) replaces the
+                                    live hit_triangle (:274-307).  NOT the reference's image:
+                                    pixels differ where the two tests disagree (tolerance in
+                                    tests/test_gpu_parity.py); bit-exact to the oracle's MT mode */
+#define PT_FLAG_ALL 63
 
 typedef struct pt_ctx pt_ctx;
 

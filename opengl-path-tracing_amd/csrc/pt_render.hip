@@ -150,6 +150,37 @@ __device__ __forceinline__ bool ray_has_nan(f3 o, f3 d) {
     return o.x != o.x || o.y != o.y || o.z != o.z || d.x != d.x || d.y != d.y || d.z != d.z;
 }
 
+// RayIntersectsTriangle (computeShader.c:228-272), Moller-Trumbore with EPSILON 1e-7: the
+// opt-in PT_FLAG_MOLLER_TRUMBORE mode (dead code in the reference, which runs hit_triangle).
+// The same operations as the oracle's mt_triangle, evaluated branch-free (the early returns
+// become a select); 1/a by the guarded exact reciprocal.  -1 for a miss.  The normal it
+// would return, normalize(cross(v1-v0, v2-v0)), is the stored per-triangle n.
+__device__ __forceinline__ float tri_mt(float4 q0, float4 q1, float4 q2, f3 o, f3 d) {
+    const float EPS = 0.0000001f;
+    const f3 v0 = mk(q0.x, q0.y, q0.z), v1 = mk(q1.x, q1.y, q1.z), v2 = mk(q2.x, q2.y, q2.z);
+    const f3 e1 = v1 - v0, e2 = v2 - v0;
+    const f3 h = pt::cross(d, e2);
+    const float a = pt::dot(e1, h);
+    bool ok = !(a > -EPS && a < EPS);
+    const float f = pt::fast_range(__builtin_fabsf(a)) ? pt::rcp_fast(a) : 1.0f / a;
+    const f3 s = o - v0;
+    const float u = f * pt::dot(s, h);
+    ok = ok && !(u < 0.0f || u > 1.0f);
+    const f3 q = pt::cross(s, e1);
+    const float v = f * pt::dot(d, q);
+    ok = ok && !(v < 0.0f || u + v > 1.0f);
+    const float t = f * pt::dot(e2, q);
+    ok = ok && t > EPS;
+    return ok ? t : -1.0f;
+}
+__device__ __forceinline__ float tri_test(int flags, const float4* T, f3 o, f3 d, float tbest, f3& n) {
+    if (flags & PT_FLAG_MOLLER_TRUMBORE) {
+        n = mk(T[0].w, T[1].w, T[2].w);
+        return tri_mt(T[0], T[1], T[2], o, d);
+    }
+    return tri_hit(T, o, d, tbest, n);
+}
+
 // calculateRayCollision (computeShader.c:367-432)
 template <bool COUNT>
 __device__ __forceinline__ bool collide(const KParams& p, f3 o, f3 d, f3& normal, f3& hitp,
@@ -192,8 +223,8 @@ __device__ __forceinline__ bool collide(const KParams& p, f3 o, f3 d, f3& normal
             int code = ~a;
             const float4* T0 = p.sc.tris + 8 * (code >> 1);
             f3 n0, n1;
-            float h1 = tri_hit(T0, o, d, t, n0);
-            float h2 = (code & 1) ? h1 : tri_hit(T0 + 4, o, d, t, n1);
+            float h1 = tri_test(p.flags, T0, o, d, t, n0);
+            float h2 = (code & 1) ? h1 : tri_test(p.flags, T0 + 4, o, d, t, n1);
             if (code & 1) n1 = n0;
             if (h1 > 0.0001f && h1 < t && (h1 < h2 || h2 < 0.0001f)) {
                 if (pt::dot(n0, d) > 0.0f) n0 = n0 * -1.0f;
@@ -449,10 +480,10 @@ __device__ __forceinline__ bool collide_v(const SceneView& S, int n_nodes, int n
             int code = ~a;
             const float4* T0 = S.tris + 8 * (code >> 1);
             f3 n0, n1;
-            float h1 = tri_hit(T0, o, d, t, n0);
+            float h1 = tri_test(flags, T0, o, d, t, n0);
             float h2 = h1;
             n1 = n0;
-            if (!(code & 1)) h2 = tri_hit(T0 + 4, o, d, t, n1);
+            if (!(code & 1)) h2 = tri_test(flags, T0 + 4, o, d, t, n1);
             if (h1 > 0.0001f && h1 < t && (h1 < h2 || h2 < 0.0001f)) {
                 if (pt::dot(n0, d) > 0.0f) n0 = n0 * -1.0f;
                 hit = true;
@@ -566,8 +597,16 @@ __device__ __forceinline__ bool collide_ww(const SceneView& S, int n_nodes, int 
             if (COUNT) { c.tri += 2; diag_tick(c.lw, c.ll); }
             const float4* T0 = S.tris + 8 * (leaf >> 1);
             f3 n0, n1;
-            float h1 = tri_hit_bf(T0, o, d, t, n0);
-            float h2 = tri_hit_bf(T0 + 4, o, d, t, n1);   // single-tri leaves hold a copy
+            float h1, h2;
+            if (flags & PT_FLAG_MOLLER_TRUMBORE) {
+                n0 = mk(T0[0].w, T0[1].w, T0[2].w);
+                n1 = mk(T0[4].w, T0[5].w, T0[6].w);
+                h1 = tri_mt(T0[0], T0[1], T0[2], o, d);
+                h2 = tri_mt(T0[4], T0[5], T0[6], o, d);
+            } else {
+                h1 = tri_hit_bf(T0, o, d, t, n0);
+                h2 = tri_hit_bf(T0 + 4, o, d, t, n1);   // single-tri leaves hold a copy
+            }
             bool c1 = h1 > 0.0001f && h1 < t && (h1 < h2 || h2 < 0.0001f);
             bool c2 = !c1 && h2 > 0.0001f && h2 < t;
             if (c1 || c2) {
@@ -1084,8 +1123,15 @@ __global__ __launch_bounds__(256, MINW) void k_render_sm(KParams p) {
                 const int code = ~leaf;                      // (slot << 1) | single
                 const int s0 = code & ~1;                    // slots 2k, 2k+1
                 f3 n0, n1;
-                float h1 = tri_hit_lazy<LDS>(S, s0, o, d, t, n0);
-                float h2 = tri_hit_lazy<LDS>(S, s0 + 1, o, d, t, n1);
+                float h1, h2;
+                if (p.flags & PT_FLAG_MOLLER_TRUMBORE) {   // wave-uniform
+                    h1 = tri_mt(tri_quad<LDS>(S, s0, 0), tri_quad<LDS>(S, s0, 1), tri_quad<LDS>(S, s0, 2), o, d);
+                    h2 = tri_mt(tri_quad<LDS>(S, s0 + 1, 0), tri_quad<LDS>(S, s0 + 1, 1),
+                                tri_quad<LDS>(S, s0 + 1, 2), o, d);
+                } else {
+                    h1 = tri_hit_lazy<LDS>(S, s0, o, d, t, n0);
+                    h2 = tri_hit_lazy<LDS>(S, s0 + 1, o, d, t, n1);
+                }
                 bool c1 = h1 > 0.0001f && h1 < t && (h1 < h2 || h2 < 0.0001f);
                 bool c2 = !c1 && h2 > 0.0001f && h2 < t;
                 if (c1 || c2) {
@@ -1229,6 +1275,7 @@ int pt_create(const pt_config* cfg, pt_ctx** out) {
         return fail(c, PT_E_ARG, "width/height out of range");
     if (cfg->display_mode < 1 || cfg->display_mode > 4) return fail(c, PT_E_ARG, "display_mode must be 1..4");
     if (cfg->max_bounce < 0) return fail(c, PT_E_ARG, "max_bounce must be >= 0");
+    if (cfg->flags & ~PT_FLAG_ALL) return fail(c, PT_E_ARG, "unknown PT_FLAG bits");
     if (c->cfg.rank < 0 || c->cfg.rank >= c->cfg.world) return fail(c, PT_E_ARG, "rank out of range");
     int ndev = 0;
     HIPCHK(c, hipGetDeviceCount(&ndev));

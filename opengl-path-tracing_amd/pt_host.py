@@ -29,6 +29,7 @@ LIB_PATH = os.environ.get("PT_LIB") or os.path.join(PKG_DIR, "build", "libptrace
 INCLUDE_DIR = os.path.join(os.path.dirname(PKG_DIR), "include")
 
 PT_FLAG_NO_AA, PT_FLAG_NO_SKY, PT_FLAG_NO_SPHERES, PT_FLAG_NO_TRIANGLES, PT_FLAG_REF_DISPATCH = 1, 2, 4, 8, 16
+PT_FLAG_MOLLER_TRUMBORE = 32   # opt-in fast triangle test (not the reference image; see pt_api.h)
 DEFAULT_CAMERA = np.array([0, -6, 1, 0, 0, 1, 0, 0, 0, 0, 0, 0], np.float32)  # ogl_path_trace.h:53-54
 
 _ERR = {-1: "PT_E_ARG", -2: "PT_E_IO", -3: "PT_E_PARSE", -4: "PT_E_SCENE", -5: "PT_E_HIP", -6: "PT_E_STATE"}

@@ -213,6 +213,31 @@ float hit_triangle(V3 o, V3 d, const float* tri, V3& normal) { // :274-307 (live
     return -1.0f;
 }
 
+// RayIntersectsTriangle :228-272 -- Moller-Trumbore, EPSILON 1e-7.  Dead code in the
+// reference (hit_triangle is the live test); the opt-in PT_FLAG_MOLLER_TRUMBORE (flags bit 5)
+// mode of the build runs it in hit_triangle's place.
+float mt_triangle(V3 o, V3 d, const float* tri, V3& normal) {
+    const float EPS = 0.0000001f;
+    V3 v0 = ld3(tri), v1 = ld3(tri + 4), v2 = ld3(tri + 8);
+    V3 e1 = sub(v1, v0), e2 = sub(v2, v0);
+    V3 h = cross(d, e2);
+    float a = dot(e1, h);
+    if (a > -EPS && a < EPS) return -1.0f;
+    float f = 1.0f / a;
+    V3 s = sub(o, v0);
+    float u = f * dot(s, h);
+    if (u < 0.0f || u > 1.0f) return -1.0f;
+    V3 q = cross(s, e1);
+    float v = f * dot(d, q);
+    if (v < 0.0f || u + v > 1.0f) return -1.0f;
+    float t = f * dot(e2, q);
+    if (t > EPS) {
+        normal = normalize(cross(e1, e2));
+        return t;
+    }
+    return -1.0f;
+}
+
 bool bvh_intersect(const float* b, V3 o, V3 d, float cur_t) {  // :309-365
     float tmin = (b[0] - o.x) / d.x;
     float tmax = (b[4] - o.x) / d.x;
@@ -262,8 +287,14 @@ void ray_collision(const Scene& sc, V3 o, V3 d, V3& normal, V3& hit_point, bool&
         if (hb && (b[8] > -1.0f)) {
             if (cnt) cnt->tri_tests += 2;
             int t0 = (int)b[8], t1 = (int)b[9];
-            float h1 = hit_triangle(o, d, sc.tris + 16 * t0, rn);
-            float h2 = hit_triangle(o, d, sc.tris + 16 * t1, rn2);
+            float h1, h2;
+            if (flags & 32) {
+                h1 = mt_triangle(o, d, sc.tris + 16 * t0, rn);
+                h2 = mt_triangle(o, d, sc.tris + 16 * t1, rn2);
+            } else {
+                h1 = hit_triangle(o, d, sc.tris + 16 * t0, rn);
+                h2 = hit_triangle(o, d, sc.tris + 16 * t1, rn2);
+            }
             if (h1 > 0.0001f && h1 < t && (h1 < h2 || h2 < 0.0001f)) {
                 if (dot(rn, d) > 0.0f) rn = muls(rn, -1.0f);
                 hit = true;
@@ -286,7 +317,8 @@ void ray_collision(const Scene& sc, V3 o, V3 d, V3& normal, V3& hit_point, bool&
 
 // :434-501
 // flags: bit0 antiAlias off, bit1 EnvironmentEnabled off, bit2 render_spheres off,
-// bit3 render_triangles off (computeShader.c:77-82 compile-time toggles; 0 = reference).
+// bit3 render_triangles off (computeShader.c:77-82 compile-time toggles; 0 = reference),
+// bit5 Moller-Trumbore triangle test (the reference's dead RayIntersectsTriangle).
 V3 trace(const Scene& sc, V3 o, V3 d, uint32_t& state, int max_bounce, int mode, int flags,
          Counters* cnt) {
     V3 incoming = v3(0, 0, 0);
@@ -596,6 +628,18 @@ void build_links(const std::vector<Node>& tree, std::vector<Node>& mod, int cur,
 extern "C" {
 
 float oracle_logf(float x) { return o_logf(x); }
+float oracle_mt_triangle(const float* o, const float* d, const float* tri, float* normal) {
+    V3 n = v3(0, 0, 0);
+    float t = mt_triangle(v3(o[0], o[1], o[2]), v3(d[0], d[1], d[2]), tri, n);
+    normal[0] = n.x; normal[1] = n.y; normal[2] = n.z;
+    return t;
+}
+float oracle_hit_triangle(const float* o, const float* d, const float* tri, float* normal) {
+    V3 n = v3(0, 0, 0);
+    float t = hit_triangle(v3(o[0], o[1], o[2]), v3(d[0], d[1], d[2]), tri, n);
+    normal[0] = n.x; normal[1] = n.y; normal[2] = n.z;
+    return t;
+}
 float oracle_cosf(float x) { return o_cosf(x); }
 
 // Batch forms for exhaustive checks.

@@ -51,6 +51,9 @@ def lib():
         L.oracle_render_pixels.argtypes = scene + [C.c_int] * 9 + [I, I, C.c_int, F, C.c_int,
                                                                    C.c_void_p]
         L.oracle_aces_rgba8.argtypes = [F, C.c_int, U8]
+        for fn in (L.oracle_mt_triangle, L.oracle_hit_triangle):
+            fn.restype = C.c_float
+            fn.argtypes = [F, F, F, F]
         _lib = L
     return _lib
 
@@ -142,3 +145,12 @@ def aces_rgba8(img):
     out = np.zeros(img.shape[:-1] + (4,), np.uint8)
     lib().oracle_aces_rgba8(img.reshape(-1), img.size // 4, out.reshape(-1))
     return out
+
+
+def triangle_test(o, d, tri, mt=False):
+    """One triangle test (hit_triangle :274-307, or RayIntersectsTriangle :228-272 when mt)
+    -> (t, normal)."""
+    n = np.zeros(3, np.float32)
+    fn = lib().oracle_mt_triangle if mt else lib().oracle_hit_triangle
+    t = fn(np.asarray(o, np.float32), np.asarray(d, np.float32), np.ascontiguousarray(tri, np.float32), n)
+    return np.float32(t), n

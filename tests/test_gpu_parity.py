@@ -387,3 +387,30 @@ def test_c3_stand_in_reduced_spp_counts(big_scene):
     assert_bitwise(got, want, "large scene, counting")
     assert [cnt["segments"], cnt["node_visits"], cnt["tri_tests"], cnt["sphere_tests"], cnt["hits"]] == \
         [int(x) for x in want_cnt]
+
+
+@pytest.mark.parametrize("extra", [0, H.PT_FLAG_NO_SPHERES])
+def test_moller_trumbore_mode_bitwise(cornell_scene, ship_scene, V, extra):
+    """Opt-in PT_FLAG_MOLLER_TRUMBORE (the reference's dead RayIntersectsTriangle, :228-272):
+    bit-exact against the oracle's MT mode on every kernel variant."""
+    flags = H.PT_FLAG_MOLLER_TRUMBORE | extra
+    for sc in (cornell_scene, ship_scene):
+        want = O.render(sc, 40, 30, max_bounce=8, n_frames=3, flags=flags)
+        got = gpu_render(sc, 40, 30, max_bounce=8, n_frames=3, flags=flags, variant=V)
+        assert_bitwise(got, want, "MT flags %d" % flags)
+
+
+def test_moller_trumbore_mode_tolerance(cornell_scene):
+    """MT vs the live hit_triangle: not the reference's image (t differs in the last bits, and
+    MT accepts edge/degenerate cases hit_triangle rejects), but the same picture.  Stated
+    tolerance after 64 frames at 96x72: relative mean |dRGB| <= 2% of the mean radiance and
+    the mean images agree to 2% per channel."""
+    ref = gpu_render(cornell_scene, 96, 72, max_bounce=8, n_frames=64)[..., :3]
+    mt = gpu_render(cornell_scene, 96, 72, max_bounce=8, n_frames=64, flags=H.PT_FLAG_MOLLER_TRUMBORE)[..., :3]
+    assert np.all(np.isfinite(mt))
+    differ = float((mt.view(np.uint32) != ref.view(np.uint32)).any(-1).mean())
+    assert differ > 0, "the MT flag did not reach the kernel"
+    rel = float(np.abs(mt - ref).mean() / np.abs(ref).mean())
+    print("MT: %.4f of pixels differ, relative mean |dRGB| = %.2e" % (differ, rel))
+    assert rel <= 0.02
+    assert np.allclose(mt.mean(axis=(0, 1)), ref.mean(axis=(0, 1)), rtol=0.02)

@@ -27,9 +27,10 @@ def main():
     ap.add_argument("--bounces", type=int, default=8)
     ap.add_argument("--tunings", default="0:0", help="leaf:shade[:adaptive[:waves[:group]]] for variants 0/3, comma list")
     ap.add_argument("--world", type=int, default=1, help="render rank 0 of a WORLD-way row split (per-GPU share)")
+    ap.add_argument("--flags", type=int, default=0, help="PT_FLAG_* bits (32 = Moller-Trumbore mode)")
     a = ap.parse_args()
     sb = pt_host.setupBuffers(*pt_scenes.write_scene(a.scene, os.path.join(REPO, "scenes")))
-    pt = pt_host.PathTracer(a.width, a.height, max_bounce=a.bounces, rank=0, world=a.world)
+    pt = pt_host.PathTracer(a.width, a.height, max_bounce=a.bounces, rank=0, world=a.world, flags=a.flags)
     pt.upload(sb)
     seg = {}
     configs = [(int(v), int(c), tu) for v in a.variants.split(",") for c in a.chunks.split(",")
