@@ -65,6 +65,10 @@ struct KParams {
     int group;
     float* rgb;                    // 3 floats per (frame, pixel)
     float rW, rH;                  // RN(1/W), RN(1/H) (host IEEE division) for the camera ray
+    // root box (min.x, max.x, min.y, max.y, min.z, max.z) and its first child (-1: the root is
+    // a leaf): a ray starting inside the root box hits it, so the walk may start at the child
+    float root_box[6];
+    int root_child;
 };
 
 // Progressive mode (hipGraph replay): the frame range comes from a device counter, and
@@ -401,11 +405,22 @@ struct SceneView {
 // planes -- node half h of node i at [h*np + i], triangle quad k of slot s at [k*tp + s] --
 // so random per-lane gathers of one half/quad hit 16-B bank groups spread over all 64
 // banks instead of every 2nd (nodes, 32-B stride) or 4th (triangles, 64-B stride) group.
+// In the LDS copy the node links are byte offsets (16 * index; -1 and leaf codes stay), so
+// a walk step addresses its node without a shift.
 extern __shared__ float4 g_lds[];   // the state-machine kernel's scene copy (nodes first)
 template <bool LDS>
 __device__ __forceinline__ void node_at(const SceneView& S, int i, float4& lo, float4& hi) {
-    if (LDS) { lo = g_lds[i]; hi = g_lds[i + S.np]; }   // LDS base 0: no address add
-    else { lo = S.nodes[2 * i]; hi = S.nodes[2 * i + 1]; }
+    if (LDS) {      // i = byte offset from the LDS base, which is 0 (checked at kernel entry)
+        typedef float v4f __attribute__((ext_vector_type(4)));
+        typedef __attribute__((address_space(3))) const v4f lds_v4f;
+        const v4f x = *(lds_v4f*)(size_t)(unsigned)i;
+        const v4f y = *(lds_v4f*)(size_t)(unsigned)(i + (S.np << 4));
+        lo = make_float4(x.x, x.y, x.z, x.w);
+        hi = make_float4(y.x, y.y, y.z, y.w);
+    } else {
+        lo = S.nodes[2 * i];
+        hi = S.nodes[2 * i + 1];
+    }
 }
 template <bool LDS>
 __device__ __forceinline__ float4 tri_quad(const SceneView& S, int slot, int k) {
@@ -825,30 +840,45 @@ __device__ __forceinline__ void trav_walk(const SceneView& S, f3 o, f3 d, f3 rd,
                                           unsigned long long live, int leaf_thresh, int shade_thresh,
                                           int& st, int& bi, int& leaf, Cnt& c) {
     const int min_thresh = leaf_thresh < shade_thresh ? leaf_thresh : shade_thresh;
+    // Inside the walk one register carries the lane's state: w >= 0 the next node, w == -1
+    // the chain ended (-> SHADE), w <= -2 stopped at a hit leaf whose continuation is
+    // -3 - w (-> LEAF).  st / bi are written back once at the end.
+    const bool walking = st == ST_TRAV;
+    const unsigned long long mw = __ballot(walking);
+    const unsigned long long pre_leaf = __ballot(st == ST_LEAF), pre_shade = __ballot(st == ST_SHADE);
+    int w = walking ? bi : -1;
     auto step = [&]() {
-        if (st == ST_TRAV) {
+        if (w >= 0) {
             float4 lo, hi;
-            node_at<LDS>(S, bi, lo, hi);
+            node_at<LDS>(S, w, lo, hi);
             int a = __float_as_int(hi.z), b = __float_as_int(hi.w);
             bool hb = (ALL_FAST || fast) ? slab_fast(lo, hi, o, d, rd, t) : slab(lo, hi, o, d, t);
             if (COUNT) { c.nodes++; diag_tick(c.tw, c.tl); }
-            const bool internal = a >= 0;      // one compare feeds both selects
-            bi = (hb && internal) ? a : b;
             leaf = a;
-            st = (hb && !internal) ? ST_LEAF : (bi < 0 ? ST_SHADE : ST_TRAV);
+            w = hb ? (a >= 0 ? a : -3 - b) : b;
         }
     };
     for (;;) {
 #pragma unroll
         for (int u = 0; u < kWalkUnroll; u++) step();
-        unsigned long long mt = __ballot(st == ST_TRAV);
+        unsigned long long mt = __ballot(w >= 0);
         if (!mt) break;
         if (__popcll(live & ~mt) >= min_thresh) {
-            if (__popcll(__ballot(st == ST_LEAF)) >= leaf_thresh) break;
-            if (__popcll(__ballot(st == ST_SHADE)) >= shade_thresh) break;
+            if (__popcll(pre_leaf | __ballot(w <= -2)) >= leaf_thresh) break;
+            if (__popcll(pre_shade | (__ballot(w == -1) & mw)) >= shade_thresh) break;
         }
     }
+    if (walking) {
+        st = w >= 0 ? ST_TRAV : (w == -1 ? ST_SHADE : ST_LEAF);
+        bi = w >= -1 ? w : -3 - w;
+    }
 }
+
+#ifdef PT_PHASE_CLOCK
+// experiment builds only (tools/ab_build.sh with PT_EXTRA=-DPT_PHASE_CLOCK): per-phase
+// wave-clock accounting of the state machine, read back by pt_debug_phase_clock
+__device__ unsigned long long g_phase_clk[6];
+#endif
 
 template <bool COUNT, bool LDS, int MINW, bool MULTI, bool SPLIT>
 __global__ __launch_bounds__(256, MINW) void k_render_sm(KParams p) {
@@ -856,9 +886,19 @@ __global__ __launch_bounds__(256, MINW) void k_render_sm(KParams p) {
     extern __shared__ float4 lds[];
     SceneView S;
     if (LDS) {      // planes (see node_at / tri_quad)
+        // node_at addresses LDS by raw offset: the dynamic LDS block must start at offset 0
+        if ((unsigned)(size_t)(__attribute__((address_space(3))) const char*)g_lds != 0u) __builtin_trap();
         const int N = p.sc.n_nodes, T = p.n_slots, nn = 2 * N, nt = 4 * T;
         const int nm = 3 * p.n_mats, ns = 2 * p.sc.n_spheres;
-        for (int i = threadIdx.x; i < nn; i += blockDim.x) lds[(i & 1) * N + (i >> 1)] = p.sc.nodes[i];
+        for (int i = threadIdx.x; i < nn; i += blockDim.x) {
+            float4 v = p.sc.nodes[i];
+            if (i & 1) {        // links -> byte offsets (see node_at)
+                const int a = __float_as_int(v.z), b = __float_as_int(v.w);
+                v.z = __int_as_float(a >= 0 ? a << 4 : a);
+                v.w = __int_as_float(b >= 0 ? b << 4 : b);
+            }
+            lds[(i & 1) * N + (i >> 1)] = v;
+        }
         for (int i = threadIdx.x; i < nt; i += blockDim.x) lds[nn + (i & 3) * T + (i >> 2)] = p.sc.tris[i];
         for (int i = threadIdx.x; i < nm; i += blockDim.x) lds[nn + nt + i] = p.sc.mats[i];
         for (int i = threadIdx.x; i < ns; i += blockDim.x) lds[nn + nt + nm + i] = p.sc.spheres[i];
@@ -884,6 +924,9 @@ __global__ __launch_bounds__(256, MINW) void k_render_sm(KParams p) {
     const unsigned total_ids = (unsigned)tiles_x * (unsigned)((p.rows_local + 7) >> 3) * n_groups * 64u;
     const int n_nodes = p.sc.n_nodes;
     const bool use_tris = !(p.flags & PT_FLAG_NO_TRIANGLES) && n_nodes > 0;
+    // walk start for a ray inside the root box: its first child (the counting build walks
+    // from the root, so the counts stay the reference's)
+    const int root_skip = (COUNT || p.root_child < 0) ? -1 : (LDS ? p.root_child << 4 : p.root_child);
 
     Cnt c = {0, 0, 0, 0, 0};
     int st = ST_SHADE;
@@ -907,11 +950,20 @@ __global__ __launch_bounds__(256, MINW) void k_render_sm(KParams p) {
     float t = 0.0f;
     int hprim = -1, bi = -1, leaf = 0;
 
+#ifdef PT_PHASE_CLOCK
+    unsigned long long clk[6] = {0, 0, 0, 0, 0, 0};   // cycles + wave iterations per phase
+#endif
     for (;;) {
         int nS = __popcll(__ballot(st == ST_SHADE));
         int nL = __popcll(__ballot(st == ST_LEAF));
         int nT = __popcll(__ballot(st == ST_TRAV));
         if (nS + nL + nT == 0) break;
+#ifdef PT_PHASE_CLOCK
+        const unsigned long long clk_t0 = clock64();
+        int clk_ph = 2;
+        if (nS > 0 && (nS >= p.shade_thresh || (nT == 0 && nL == 0))) clk_ph = 0;
+        else if (nL > 0 && (nL >= p.leaf_thresh || nT == 0)) clk_ph = 1;
+#endif
         if (nS > 0 && (nS >= p.shade_thresh || (nT == 0 && nL == 0))) {
             // ---------------- SHADE: finish segment, regenerate, set up next segment
             if (st == ST_SHADE && !fresh) {
@@ -1113,7 +1165,12 @@ __global__ __launch_bounds__(256, MINW) void k_render_sm(KParams p) {
                 }
                 fresh = false;
                 const bool walk = use_tris && (COUNT || !ray_has_nan(o, d));
-                bi = walk ? 0 : -1;
+                // inside the root box (all three axes, inclusive) each axis has near <= 0 <=
+                // far, so the exact slab says hit for any t >= 0: skip the root's test
+                const bool inside = root_skip >= 0 && fast && o.x >= p.root_box[0] && o.x <= p.root_box[1] &&
+                                    o.y >= p.root_box[2] && o.y <= p.root_box[3] && o.z >= p.root_box[4] &&
+                                    o.z <= p.root_box[5];
+                bi = walk ? (inside ? root_skip : 0) : -1;
                 st = walk ? ST_TRAV : ST_SHADE;
             }
         } else if (nL > 0 && (nL >= p.leaf_thresh || nT == 0)) {
@@ -1153,7 +1210,15 @@ __global__ __launch_bounds__(256, MINW) void k_render_sm(KParams p) {
                 trav_walk<false, COUNT, LDS>(S, o, d, rd, fast, t, live, p.leaf_thresh, p.shade_thresh, st, bi,
                                         leaf, c);
         }
+#ifdef PT_PHASE_CLOCK
+        clk[clk_ph] += clock64() - clk_t0;
+        clk[3 + clk_ph] += 1;
+#endif
     }
+#ifdef PT_PHASE_CLOCK
+    if (lane == 0)
+        for (int i = 0; i < 6; i++) atomicAdd(&g_phase_clk[i], clk[i]);
+#endif
     flush_counters<COUNT>(p, c);
 }
 
@@ -1223,6 +1288,8 @@ struct pt_ctx {
     hipGraphExec_t graph_exec = nullptr;
     int graph_frames = 0;
     int n_nodes = 0, n_spheres = 0, n_mats = 0, n_slots = 0, scene_fast = 0;
+    float root_box[6] = {0, 0, 0, 0, 0, 0};
+    int root_child = -1;
     size_t lds_bytes = 0;
     unsigned persist_blocks = 2048;
     // 0 = automatic: 32/48 when the scene is staged in LDS (best on C2), 16/32 when the walk
@@ -1463,6 +1530,15 @@ int pt_upload_scene(pt_ctx* c, const float* tris, int n_tris, const float* bvh, 
         }
     }
     c->lds_bytes = (size_t)(2 * n_nodes + 4 * c->n_slots + 3 * n_mats + 2 * n_spheres) * sizeof(float4);
+    c->root_child = -1;
+    if (n_nodes > 0) {
+        const float4 r0 = dn[0], r1 = dn[1];
+        const float box[6] = {r0.x, r0.y, r0.z, r0.w, r1.x, r1.y};
+        std::memcpy(c->root_box, box, sizeof(box));
+        int a;
+        std::memcpy(&a, &r1.z, 4);
+        c->root_child = a >= 0 ? a : -1;
+    }
     c->scene_ok = true;
     return PT_OK;
 }
@@ -1594,6 +1670,8 @@ static int enqueue_render(pt_ctx* c, int frame_first, int n_frames, int acc_firs
     p.n_slots = c->n_slots;
     p.n_mats = c->n_mats;
     p.scene_fast = c->scene_fast;
+    std::memcpy(p.root_box, c->root_box, sizeof(p.root_box));
+    p.root_child = c->root_child;
     {
         bool lds_scene = c->lds_bytes <= kLdsSceneMax && c->variant != 3;
         p.leaf_thresh = c->leaf_thresh ? c->leaf_thresh : (lds_scene ? 32 : 16);
@@ -1865,6 +1943,18 @@ int pt_stream(pt_ctx* c, void** s) {
     *s = (void*)c->stream;
     return PT_OK;
 }
+
+#ifdef PT_PHASE_CLOCK
+extern "C" int pt_debug_phase_clock(unsigned long long out[6], int reset) {
+    if (hipDeviceSynchronize() != hipSuccess) return -1;
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_phase_clk), sizeof(unsigned long long) * 6) != hipSuccess) return -1;
+    if (reset) {
+        unsigned long long z[6] = {0, 0, 0, 0, 0, 0};
+        if (hipMemcpyToSymbol(HIP_SYMBOL(g_phase_clk), z, sizeof(z)) != hipSuccess) return -1;
+    }
+    return 0;
+}
+#endif
 
 int pt_stats_ex(pt_ctx* c, unsigned long long out[16]) {
     if (!c || !out) return PT_E_ARG;

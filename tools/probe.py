@@ -6,6 +6,7 @@ Prints Mrays/s and kernel ms per configuration; segment counts come from a count
 import argparse
 import os
 import sys
+import ctypes
 import time
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -13,6 +14,20 @@ sys.path.insert(0, os.path.join(REPO, "opengl-path-tracing_amd"))
 
 import pt_host  # noqa: E402
 import pt_scenes  # noqa: E402
+
+
+def phase_clock(segments):
+    """Experiment builds with -DPT_PHASE_CLOCK: wave-clock share per state-machine phase."""
+    fn = getattr(pt_host.lib(), "pt_debug_phase_clock", None)
+    if fn is None:
+        return
+    out = (ctypes.c_ulonglong * 6)()
+    fn(out, 1)
+    tot = float(sum(out[:3])) or 1.0
+    print("  phase clock: shade %.3f leaf %.3f trav %.3f | wave-iters/segment shade %.4f leaf %.4f trav %.4f"
+          " | clk per wave-iter %.0f %.0f %.0f" % (
+              out[0] / tot, out[1] / tot, out[2] / tot, out[3] / segments, out[4] / segments, out[5] / segments,
+              out[0] / max(out[3], 1), out[1] / max(out[4], 1), out[2] / max(out[5], 1)), flush=True)
 
 
 def main():
@@ -68,6 +83,7 @@ def main():
             kms, n = pt.timing(reset=True)
             print("round %d variant %d chunk %4d tune %-6s: %8.1f Mrays/s  wall %.1f ms  kernel %.1f ms (%d launches)  %.3f ms/frame"
                   % (rnd, v, c, tu, seg[(v, c, tu)] / dt / 1e6, dt * 1e3, kms, n, dt * 1e3 / a.spp), flush=True)
+            phase_clock(seg[(v, c, tu)])
     pt.close()
 
 
