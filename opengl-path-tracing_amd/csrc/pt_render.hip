@@ -34,6 +34,9 @@ namespace {
 
 struct DevScene {
     const float4* nodes;
+    // the state-machine kernel's LDS image of the same tree (pt_upload_scene): node planes
+    // with WalkLinks (byte offsets, 16 * index)
+    const float4* walk_lds;
     const float4* tris;
     const float4* mats;
     const float4* spheres;
@@ -405,14 +408,22 @@ struct SceneView {
 // planes -- node half h of node i at [h*np + i], triangle quad k of slot s at [k*tp + s] --
 // so random per-lane gathers of one half/quad hit 16-B bank groups spread over all 64
 // banks instead of every 2nd (nodes, 32-B stride) or 4th (triangles, 64-B stride) group.
-// In the LDS copy the node links are byte offsets (16 * index; -1 and leaf codes stay), so
-// a walk step addresses its node without a shift.
+//
+// WalkLinks: in the LDS image a node's (hi.z, hi.w) are the walk's next position after a
+// box hit and after a miss, as byte offsets of the node (16 * index, its lo-plane entry) or
+// -1 (chain ends):
+//   internal node: (first child, next-right)
+//   leaf node:     (-2 - code, next-right), code = slot << 1 | single: a hit stops the walk
+// so one select is the whole link step.  The leaf's continuation (its next-right) rides in
+// the spare .z of its first triangle's 4th quad, which the leaf test loads anyway.
+// The global-memory walk keeps the reference links (node indices, a = ~code at a leaf):
+// there the loads, not the selects, set the pace, and the reference form measured faster.
 extern __shared__ float4 g_lds[];   // the state-machine kernel's scene copy (nodes first)
+typedef float v4f __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) const v4f lds_v4f;
 template <bool LDS>
 __device__ __forceinline__ void node_at(const SceneView& S, int i, float4& lo, float4& hi) {
     if (LDS) {      // i = byte offset from the LDS base, which is 0 (checked at kernel entry)
-        typedef float v4f __attribute__((ext_vector_type(4)));
-        typedef __attribute__((address_space(3))) const v4f lds_v4f;
         const v4f x = *(lds_v4f*)(size_t)(unsigned)i;
         const v4f y = *(lds_v4f*)(size_t)(unsigned)(i + (S.np << 4));
         lo = make_float4(x.x, x.y, x.z, x.w);
@@ -422,6 +433,7 @@ __device__ __forceinline__ void node_at(const SceneView& S, int i, float4& lo, f
         hi = S.nodes[2 * i + 1];
     }
 }
+
 template <bool LDS>
 __device__ __forceinline__ float4 tri_quad(const SceneView& S, int slot, int k) {
     return LDS ? S.tris[slot + k * S.tp] : S.tris[4 * slot + k];
@@ -540,9 +552,10 @@ __device__ __forceinline__ float tri_hit_bf(const float4* T, f3 o, f3 d, float t
 // lane of the wave still needs them (a wave-uniform skip; per lane the verdict is the
 // same select as tri_hit_bf, so the bits are identical).
 template <bool LDS>
-__device__ __forceinline__ float tri_hit_lazy(const SceneView& S, int slot, f3 o, f3 d, float tbest, f3& n) {
+__device__ __forceinline__ float tri_hit_lazy(const SceneView& S, int slot, float4 q3, f3 o, f3 d, float tbest,
+                                              f3& n) {
     float4 q0 = tri_quad<LDS>(S, slot, 0), q1 = tri_quad<LDS>(S, slot, 1);
-    float4 q2 = tri_quad<LDS>(S, slot, 2), q3 = tri_quad<LDS>(S, slot, 3);
+    float4 q2 = tri_quad<LDS>(S, slot, 2);      // q3: loaded by the caller
     n = mk(q0.w, q1.w, q2.w);
     float t = -(pt::dot(n, o) + q3.x) / pt::dot(n, d);
     bool ok = !(t < 0.0f) && (t < tbest);
@@ -840,9 +853,9 @@ __device__ __forceinline__ void trav_walk(const SceneView& S, f3 o, f3 d, f3 rd,
                                           unsigned long long live, int leaf_thresh, int shade_thresh,
                                           int& st, int& bi, int& leaf, Cnt& c) {
     const int min_thresh = leaf_thresh < shade_thresh ? leaf_thresh : shade_thresh;
-    // Inside the walk one register carries the lane's state: w >= 0 the next node, w == -1
-    // the chain ended (-> SHADE), w <= -2 stopped at a hit leaf whose continuation is
-    // -3 - w (-> LEAF).  st / bi are written back once at the end.
+    // Inside the walk one register carries the lane's state (WalkLinks): w >= 0 the next
+    // node, w == -1 the chain ended (-> SHADE), w <= -2 stopped at the hit leaf with code
+    // -2 - w (-> LEAF, bi = w).  st / bi are written back once at the end.
     const bool walking = st == ST_TRAV;
     const unsigned long long mw = __ballot(walking);
     const unsigned long long pre_leaf = __ballot(st == ST_LEAF), pre_shade = __ballot(st == ST_SHADE);
@@ -854,8 +867,15 @@ __device__ __forceinline__ void trav_walk(const SceneView& S, f3 o, f3 d, f3 rd,
             int a = __float_as_int(hi.z), b = __float_as_int(hi.w);
             bool hb = (ALL_FAST || fast) ? slab_fast(lo, hi, o, d, rd, t) : slab(lo, hi, o, d, t);
             if (COUNT) { c.nodes++; diag_tick(c.tw, c.tl); }
-            leaf = a;
-            w = hb ? (a >= 0 ? a : -3 - b) : b;
+#ifdef PT_PHASE_CLOCK
+            if (!COUNT) diag_tick(c.tw, c.tl);
+#endif
+            if (LDS) {
+                w = hb ? a : b;                       // WalkLinks: one select
+            } else {                                  // reference links: a = ~code at a leaf
+                leaf = a;
+                w = hb ? (a >= 0 ? a : -3 - b) : b;
+            }
         }
     };
     for (;;) {
@@ -870,14 +890,19 @@ __device__ __forceinline__ void trav_walk(const SceneView& S, f3 o, f3 d, f3 rd,
     }
     if (walking) {
         st = w >= 0 ? ST_TRAV : (w == -1 ? ST_SHADE : ST_LEAF);
-        bi = w >= -1 ? w : -3 - w;
+        if (LDS) {
+            bi = w;
+            leaf = -2 - w;                // the leaf's code
+        } else {
+            bi = w >= -1 ? w : -3 - w;    // the leaf's continuation; leaf = ~code
+        }
     }
 }
 
 #ifdef PT_PHASE_CLOCK
 // experiment builds only (tools/ab_build.sh with PT_EXTRA=-DPT_PHASE_CLOCK): per-phase
 // wave-clock accounting of the state machine, read back by pt_debug_phase_clock
-__device__ unsigned long long g_phase_clk[6];
+__device__ unsigned long long g_phase_clk[8];
 #endif
 
 template <bool COUNT, bool LDS, int MINW, bool MULTI, bool SPLIT>
@@ -890,15 +915,7 @@ __global__ __launch_bounds__(256, MINW) void k_render_sm(KParams p) {
         if ((unsigned)(size_t)(__attribute__((address_space(3))) const char*)g_lds != 0u) __builtin_trap();
         const int N = p.sc.n_nodes, T = p.n_slots, nn = 2 * N, nt = 4 * T;
         const int nm = 3 * p.n_mats, ns = 2 * p.sc.n_spheres;
-        for (int i = threadIdx.x; i < nn; i += blockDim.x) {
-            float4 v = p.sc.nodes[i];
-            if (i & 1) {        // links -> byte offsets (see node_at)
-                const int a = __float_as_int(v.z), b = __float_as_int(v.w);
-                v.z = __int_as_float(a >= 0 ? a << 4 : a);
-                v.w = __int_as_float(b >= 0 ? b << 4 : b);
-            }
-            lds[(i & 1) * N + (i >> 1)] = v;
-        }
+        for (int i = threadIdx.x; i < nn; i += blockDim.x) lds[i] = p.sc.walk_lds[i];   // ready-made image
         for (int i = threadIdx.x; i < nt; i += blockDim.x) lds[nn + (i & 3) * T + (i >> 2)] = p.sc.tris[i];
         for (int i = threadIdx.x; i < nm; i += blockDim.x) lds[nn + nt + i] = p.sc.mats[i];
         for (int i = threadIdx.x; i < ns; i += blockDim.x) lds[nn + nt + nm + i] = p.sc.spheres[i];
@@ -910,7 +927,7 @@ __global__ __launch_bounds__(256, MINW) void k_render_sm(KParams p) {
         S.np = N;
         S.tp = T;
     } else {
-        S.nodes = p.sc.nodes;
+        S.nodes = p.sc.nodes;     // reference layout; the walk image is for LDS only
         S.tris = p.sc.tris;
         S.mats = p.sc.mats;
         S.spheres = p.sc.spheres;
@@ -926,7 +943,7 @@ __global__ __launch_bounds__(256, MINW) void k_render_sm(KParams p) {
     const bool use_tris = !(p.flags & PT_FLAG_NO_TRIANGLES) && n_nodes > 0;
     // walk start for a ray inside the root box: its first child (the counting build walks
     // from the root, so the counts stay the reference's)
-    const int root_skip = (COUNT || p.root_child < 0) ? -1 : (LDS ? p.root_child << 4 : p.root_child);
+    const int root_skip = (COUNT || p.root_child < 0) ? -1 : p.root_child << (LDS ? 4 : 0);
 
     Cnt c = {0, 0, 0, 0, 0};
     int st = ST_SHADE;
@@ -948,7 +965,7 @@ __global__ __launch_bounds__(256, MINW) void k_render_sm(KParams p) {
     bool fast = false;
     f3 rd = mk(0, 0, 0);
     float t = 0.0f;
-    int hprim = -1, bi = -1, leaf = 0;
+    int hprim = -1, bi = -1, leaf = 0;   // bi: walk position (WalkLinks); leaf: code of a hit leaf
 
 #ifdef PT_PHASE_CLOCK
     unsigned long long clk[6] = {0, 0, 0, 0, 0, 0};   // cycles + wave iterations per phase
@@ -1177,8 +1194,10 @@ __global__ __launch_bounds__(256, MINW) void k_render_sm(KParams p) {
             // ---------------- LEAF: both triangle tests + the 2-way choice (:406-429)
             if (st == ST_LEAF) {
                 if (COUNT) { c.tri += 2; diag_tick(c.lw, c.ll); }
-                const int code = ~leaf;                      // (slot << 1) | single
+                const int code = LDS ? leaf : ~leaf;         // (slot << 1) | single
                 const int s0 = code & ~1;                    // slots 2k, 2k+1
+                const float4 q3 = tri_quad<LDS>(S, s0, 3);   // .z / .w: the leaf's next-right
+                const int cont = LDS ? __float_as_int(q3.z) : bi;
                 f3 n0, n1;
                 float h1, h2;
                 if (p.flags & PT_FLAG_MOLLER_TRUMBORE) {   // wave-uniform
@@ -1186,8 +1205,8 @@ __global__ __launch_bounds__(256, MINW) void k_render_sm(KParams p) {
                     h2 = tri_mt(tri_quad<LDS>(S, s0 + 1, 0), tri_quad<LDS>(S, s0 + 1, 1),
                                 tri_quad<LDS>(S, s0 + 1, 2), o, d);
                 } else {
-                    h1 = tri_hit_lazy<LDS>(S, s0, o, d, t, n0);
-                    h2 = tri_hit_lazy<LDS>(S, s0 + 1, o, d, t, n1);
+                    h1 = tri_hit_lazy<LDS>(S, s0, q3, o, d, t, n0);
+                    h2 = tri_hit_lazy<LDS>(S, s0 + 1, tri_quad<LDS>(S, s0 + 1, 3), o, d, t, n1);
                 }
                 bool c1 = h1 > 0.0001f && h1 < t && (h1 < h2 || h2 < 0.0001f);
                 bool c2 = !c1 && h2 > 0.0001f && h2 < t;
@@ -1195,6 +1214,7 @@ __global__ __launch_bounds__(256, MINW) void k_render_sm(KParams p) {
                     t = c1 ? h1 : h2;
                     hprim = s0 + (c1 ? 0 : 1);
                 }
+                bi = cont;
                 st = bi > -1 ? ST_TRAV : ST_SHADE;
             }
         } else {
@@ -1204,11 +1224,9 @@ __global__ __launch_bounds__(256, MINW) void k_render_sm(KParams p) {
             // the per-node IEEE-division branch.
             const unsigned long long live = __ballot(st != ST_DONE);
             if (__all(fast || st != ST_TRAV))
-                trav_walk<true, COUNT, LDS>(S, o, d, rd, fast, t, live, p.leaf_thresh, p.shade_thresh, st, bi,
-                                       leaf, c);
+                trav_walk<true, COUNT, LDS>(S, o, d, rd, fast, t, live, p.leaf_thresh, p.shade_thresh, st, bi, leaf, c);
             else
-                trav_walk<false, COUNT, LDS>(S, o, d, rd, fast, t, live, p.leaf_thresh, p.shade_thresh, st, bi,
-                                        leaf, c);
+                trav_walk<false, COUNT, LDS>(S, o, d, rd, fast, t, live, p.leaf_thresh, p.shade_thresh, st, bi, leaf, c);
         }
 #ifdef PT_PHASE_CLOCK
         clk[clk_ph] += clock64() - clk_t0;
@@ -1218,6 +1236,10 @@ __global__ __launch_bounds__(256, MINW) void k_render_sm(KParams p) {
 #ifdef PT_PHASE_CLOCK
     if (lane == 0)
         for (int i = 0; i < 6; i++) atomicAdd(&g_phase_clk[i], clk[i]);
+    {
+        unsigned long long tw = wave_sum(c.tw), tl = wave_sum(c.tl);
+        if (lane == 0) { atomicAdd(&g_phase_clk[6], tw); atomicAdd(&g_phase_clk[7], tl); }
+    }
 #endif
     flush_counters<COUNT>(p, c);
 }
@@ -1275,6 +1297,7 @@ struct pt_ctx {
     float4* accum = nullptr;
     uchar4* rgba8 = nullptr;
     float4 *d_nodes = nullptr, *d_tris = nullptr, *d_mats = nullptr, *d_spheres = nullptr;
+    float4* d_walk_lds = nullptr;   // LDS walk image (DevScene)
     unsigned long long* d_counters = nullptr;
     unsigned int* d_work = nullptr;
     int* d_frame = nullptr;                      // progressive graph frame counter
@@ -1324,7 +1347,8 @@ static int fail(pt_ctx* c, int code, const std::string& msg) {
 
 static void free_scene(pt_ctx* c) {
     (void)hipFree(c->d_nodes); (void)hipFree(c->d_tris); (void)hipFree(c->d_mats); (void)hipFree(c->d_spheres);
-    c->d_nodes = c->d_tris = c->d_mats = c->d_spheres = nullptr;
+    (void)hipFree(c->d_walk_lds);
+    c->d_nodes = c->d_tris = c->d_mats = c->d_spheres = c->d_walk_lds = nullptr;
     c->scene_ok = false;
 }
 
@@ -1504,8 +1528,28 @@ int pt_upload_scene(pt_ctx* c, const float* tris, int n_tris, const float* bvh, 
         ds[2 * (size_t)i] = make_float4(s[0], s[1], s[2], s[3] * s[3]);
         ds[2 * (size_t)i + 1] = make_float4(mb, 0, 0, 0);
     }
+    // LDS walk image of the state-machine kernel (WalkLinks in the kernel source): the node
+    // planes with links as byte offsets (16 * index) and a leaf's hit link -2 - code; the
+    // leaf's next-right (same scale) goes to its first triangle's quad 3 .z
+    const size_t N = (size_t)std::max(n_nodes, 1);
+    std::vector<float4> dwl(2 * N);
+    for (int i = 0; i < n_nodes; i++) {
+        float4 lo = dn[2 * (size_t)i], hi = dn[2 * (size_t)i + 1];
+        int a, b;
+        std::memcpy(&a, &hi.z, 4);
+        std::memcpy(&b, &hi.w, 4);
+        const bool leaf = a < 0;
+        int ha = leaf ? -2 - ~a : 16 * a, hb = b >= 0 ? 16 * b : -1;
+        std::memcpy(&hi.z, &ha, 4);
+        std::memcpy(&hi.w, &hb, 4);
+        dwl[i] = lo;
+        dwl[N + i] = hi;
+        if (leaf) std::memcpy(&dt[8 * (size_t)leaf_slot[i] + 3].z, &hb, 4);
+    }
     drop_graph(c);
     free_scene(c);
+    HIPCHK(c, hipMalloc(&c->d_walk_lds, dwl.size() * sizeof(float4)));
+    HIPCHK(c, hipMemcpy(c->d_walk_lds, dwl.data(), dwl.size() * sizeof(float4), hipMemcpyHostToDevice));
     HIPCHK(c, hipMalloc(&c->d_nodes, dn.size() * sizeof(float4)));
     HIPCHK(c, hipMalloc(&c->d_tris, dt.size() * sizeof(float4)));
     HIPCHK(c, hipMalloc(&c->d_mats, dm.size() * sizeof(float4)));
@@ -1642,6 +1686,7 @@ static int enqueue_render(pt_ctx* c, int frame_first, int n_frames, int acc_firs
     KParams p;
     std::memset(&p, 0, sizeof(p));
     p.sc.nodes = c->d_nodes;
+    p.sc.walk_lds = c->d_walk_lds;
     p.sc.tris = c->d_tris;
     p.sc.mats = c->d_mats;
     p.sc.spheres = c->d_spheres;
@@ -1945,11 +1990,11 @@ int pt_stream(pt_ctx* c, void** s) {
 }
 
 #ifdef PT_PHASE_CLOCK
-extern "C" int pt_debug_phase_clock(unsigned long long out[6], int reset) {
+extern "C" int pt_debug_phase_clock(unsigned long long out[8], int reset) {
     if (hipDeviceSynchronize() != hipSuccess) return -1;
-    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_phase_clk), sizeof(unsigned long long) * 6) != hipSuccess) return -1;
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_phase_clk), sizeof(unsigned long long) * 8) != hipSuccess) return -1;
     if (reset) {
-        unsigned long long z[6] = {0, 0, 0, 0, 0, 0};
+        unsigned long long z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
         if (hipMemcpyToSymbol(HIP_SYMBOL(g_phase_clk), z, sizeof(z)) != hipSuccess) return -1;
     }
     return 0;

@@ -21,13 +21,15 @@ def phase_clock(segments):
     fn = getattr(pt_host.lib(), "pt_debug_phase_clock", None)
     if fn is None:
         return
-    out = (ctypes.c_ulonglong * 6)()
+    out = (ctypes.c_ulonglong * 8)()
     fn(out, 1)
     tot = float(sum(out[:3])) or 1.0
     print("  phase clock: shade %.3f leaf %.3f trav %.3f | wave-iters/segment shade %.4f leaf %.4f trav %.4f"
           " | clk per wave-iter %.0f %.0f %.0f" % (
               out[0] / tot, out[1] / tot, out[2] / tot, out[3] / segments, out[4] / segments, out[5] / segments,
               out[0] / max(out[3], 1), out[1] / max(out[4], 1), out[2] / max(out[5], 1)), flush=True)
+    print("  walk: wave-steps %d lane-steps %d (util %.3f, lane-steps/segment %.2f)" % (
+        out[6], out[7], out[7] / max(64.0 * out[6], 1.0), out[7] / segments), flush=True)
 
 
 def main():
