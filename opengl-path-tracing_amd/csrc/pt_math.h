@@ -196,6 +196,12 @@ PT_HD uint32_t next_random(uint32_t& s) {
 }
 PT_HD float random01(uint32_t& s) { return (float)next_random(s) * (1.0f / 4294967296.0f); }
 PT_HD float random_normal(uint32_t& s) {            // :115-120 (theta first, then rho)
+#if defined(PT_EXP_HW_NORMAL) && defined(__HIP_DEVICE_COMPILE__)
+    // timing experiment only (NOT the pinned arithmetic): hardware log2 / cos
+    float u1 = random01(s);
+    float u2 = random01(s);
+    return __builtin_sqrtf(-1.3862944f * __builtin_amdgcn_logf(u2)) * __builtin_amdgcn_cosf(u1);
+#endif
     float theta = (2.0f * 3.1415926f) * random01(s);
     float rho = sqrt_g(-2.0f * logf_pinned(random01(s)));
     return rho * cosf_pinned(theta);

@@ -416,6 +416,10 @@ struct SceneView {
 //   leaf node:     (-2 - code, next-right), code = slot << 1 | single: a hit stops the walk
 // so one select is the whole link step.  The leaf's continuation (its next-right) rides in
 // the spare .z of its first triangle's 4th quad, which the leaf test loads anyway.
+// The LDS walk holds 8 such images, one per octant of ray directions (image k at byte
+// 32 * N * k, links absolute inside their image): image k stores the bounds of each axis
+// whose direction sign bit is set in k swapped, near bound first (slab_oct); image 0 is the
+// reference order.  A leaf's continuation is stored as its image-0 offset.
 // The global-memory walk keeps the reference links (node indices, a = ~code at a leaf):
 // there the loads, not the selects, set the pace, and the reference form measured faster.
 extern __shared__ float4 g_lds[];   // the state-machine kernel's scene copy (nodes first)
@@ -461,6 +465,31 @@ __device__ __forceinline__ bool slab_fast(float4 A, float4 B, f3 o, f3 d, f3 rd,
     float tn = fmaxf(fmaxf(fminf(x0, x1), fminf(y0, y1)), fminf(z0, z1));
     float tf = fminf(fminf(fmaxf(x0, x1), fmaxf(y0, y1)), fmaxf(z0, z1));
     return tn <= tf && tn <= cur_t;
+}
+
+// Slab test on an octant image of the LDS walk (WalkLinks): the node's bounds are stored
+// near-first for the ray's direction signs, so the per-axis min/max of slab_fast is known
+// in advance.  Equal to slab_fast for boxes with min <= max on every axis (checked at upload
+// as part of the scene half of the guard): for d_i > 0 RN((min-o)/d) <= RN((max-o)/d) and for
+// d_i < 0 the reverse (RN and the subtraction are monotone), so the near quotient IS the
+// minimum; values only enter comparisons, where -0 == +0.
+__device__ __forceinline__ bool slab_oct(float4 A, float4 B, f3 o, f3 d, f3 rd, float cur_t) {
+    float xn = qdiv(A.x - o.x, d.x, rd.x), xf = qdiv(A.y - o.x, d.x, rd.x);
+    float yn = qdiv(A.z - o.y, d.y, rd.y), yf = qdiv(A.w - o.y, d.y, rd.y);
+    float zn = qdiv(B.x - o.z, d.z, rd.z), zf = qdiv(B.y - o.z, d.z, rd.z);
+    float tn = fmaxf(fmaxf(xn, yn), zn);
+    float tf = fminf(fminf(xf, yf), zf);
+    return tn <= tf && tn <= cur_t;
+}
+
+// Byte offset of the ray's octant image in the LDS walk: image k = sx | sy << 1 | sz << 2
+// holds the nodes with the bounds of each axis whose direction is negative swapped.  Only
+// for rays inside the exact-reciprocal guard (d_i != 0, finite); other rays walk image 0
+// (the reference order) with the reference slab.
+__device__ __forceinline__ int oct_base(f3 d, int img_bytes) {
+    const unsigned o = (__float_as_uint(d.x) >> 31) | ((__float_as_uint(d.y) >> 30) & 2u) |
+                       ((__float_as_uint(d.z) >> 29) & 4u);
+    return (int)o * img_bytes;
 }
 
 template <bool COUNT>
@@ -865,7 +894,8 @@ __device__ __forceinline__ void trav_walk(const SceneView& S, f3 o, f3 d, f3 rd,
             float4 lo, hi;
             node_at<LDS>(S, w, lo, hi);
             int a = __float_as_int(hi.z), b = __float_as_int(hi.w);
-            bool hb = (ALL_FAST || fast) ? slab_fast(lo, hi, o, d, rd, t) : slab(lo, hi, o, d, t);
+            bool hb = (ALL_FAST || fast) ? (LDS ? slab_oct(lo, hi, o, d, rd, t) : slab_fast(lo, hi, o, d, rd, t))
+                                         : slab(lo, hi, o, d, t);
             if (COUNT) { c.nodes++; diag_tick(c.tw, c.tl); }
 #ifdef PT_PHASE_CLOCK
             if (!COUNT) diag_tick(c.tw, c.tl);
@@ -913,7 +943,7 @@ __global__ __launch_bounds__(256, MINW) void k_render_sm(KParams p) {
     if (LDS) {      // planes (see node_at / tri_quad)
         // node_at addresses LDS by raw offset: the dynamic LDS block must start at offset 0
         if ((unsigned)(size_t)(__attribute__((address_space(3))) const char*)g_lds != 0u) __builtin_trap();
-        const int N = p.sc.n_nodes, T = p.n_slots, nn = 2 * N, nt = 4 * T;
+        const int N = p.sc.n_nodes, T = p.n_slots, nn = 16 * N, nt = 4 * T;   // 8 octant images
         const int nm = 3 * p.n_mats, ns = 2 * p.sc.n_spheres;
         for (int i = threadIdx.x; i < nn; i += blockDim.x) lds[i] = p.sc.walk_lds[i];   // ready-made image
         for (int i = threadIdx.x; i < nt; i += blockDim.x) lds[nn + (i & 3) * T + (i >> 2)] = p.sc.tris[i];
@@ -1187,7 +1217,8 @@ __global__ __launch_bounds__(256, MINW) void k_render_sm(KParams p) {
                 const bool inside = root_skip >= 0 && fast && o.x >= p.root_box[0] && o.x <= p.root_box[1] &&
                                     o.y >= p.root_box[2] && o.y <= p.root_box[3] && o.z >= p.root_box[4] &&
                                     o.z <= p.root_box[5];
-                bi = walk ? (inside ? root_skip : 0) : -1;
+                const int img = (LDS && fast) ? oct_base(d, S.np << 5) : 0;   // octant image
+                bi = walk ? (inside ? root_skip : 0) + img : -1;
                 st = walk ? ST_TRAV : ST_SHADE;
             }
         } else if (nL > 0 && (nL >= p.leaf_thresh || nT == 0)) {
@@ -1197,7 +1228,8 @@ __global__ __launch_bounds__(256, MINW) void k_render_sm(KParams p) {
                 const int code = LDS ? leaf : ~leaf;         // (slot << 1) | single
                 const int s0 = code & ~1;                    // slots 2k, 2k+1
                 const float4 q3 = tri_quad<LDS>(S, s0, 3);   // .z / .w: the leaf's next-right
-                const int cont = LDS ? __float_as_int(q3.z) : bi;
+                int cont = LDS ? __float_as_int(q3.z) : bi;      // LDS: offset in image 0
+                if (LDS && fast && cont >= 0) cont += oct_base(d, S.np << 5);
                 f3 n0, n1;
                 float h1, h2;
                 if (p.flags & PT_FLAG_MOLLER_TRUMBORE) {   // wave-uniform
@@ -1528,23 +1560,30 @@ int pt_upload_scene(pt_ctx* c, const float* tris, int n_tris, const float* bvh, 
         ds[2 * (size_t)i] = make_float4(s[0], s[1], s[2], s[3] * s[3]);
         ds[2 * (size_t)i + 1] = make_float4(mb, 0, 0, 0);
     }
-    // LDS walk image of the state-machine kernel (WalkLinks in the kernel source): the node
-    // planes with links as byte offsets (16 * index) and a leaf's hit link -2 - code; the
-    // leaf's next-right (same scale) goes to its first triangle's quad 3 .z
+    // LDS walk images of the state-machine kernel (WalkLinks in the kernel source): per ray
+    // octant k the node planes (bounds of the axes whose bit is set in k swapped) with links
+    // as byte offsets (16 * (2N * k + index)) and a leaf's hit link -2 - code; the leaf's
+    // next-right (image-0 offset) goes to its first triangle's quad 3 .z
     const size_t N = (size_t)std::max(n_nodes, 1);
-    std::vector<float4> dwl(2 * N);
-    for (int i = 0; i < n_nodes; i++) {
-        float4 lo = dn[2 * (size_t)i], hi = dn[2 * (size_t)i + 1];
-        int a, b;
-        std::memcpy(&a, &hi.z, 4);
-        std::memcpy(&b, &hi.w, 4);
-        const bool leaf = a < 0;
-        int ha = leaf ? -2 - ~a : 16 * a, hb = b >= 0 ? 16 * b : -1;
-        std::memcpy(&hi.z, &ha, 4);
-        std::memcpy(&hi.w, &hb, 4);
-        dwl[i] = lo;
-        dwl[N + i] = hi;
-        if (leaf) std::memcpy(&dt[8 * (size_t)leaf_slot[i] + 3].z, &hb, 4);
+    std::vector<float4> dwl(16 * N);
+    for (int k = 0; k < 8; k++) {
+        const int base = 16 * 2 * (int)N * k;
+        for (int i = 0; i < n_nodes; i++) {
+            float4 lo = dn[2 * (size_t)i], hi = dn[2 * (size_t)i + 1];
+            int a, b;
+            std::memcpy(&a, &hi.z, 4);
+            std::memcpy(&b, &hi.w, 4);
+            const bool leaf = a < 0;
+            int ha = leaf ? -2 - ~a : base + 16 * a, hb = b >= 0 ? base + 16 * b : -1;
+            std::memcpy(&hi.z, &ha, 4);
+            std::memcpy(&hi.w, &hb, 4);
+            if (k & 1) std::swap(lo.x, lo.y);
+            if (k & 2) std::swap(lo.z, lo.w);
+            if (k & 4) std::swap(hi.x, hi.y);
+            dwl[2 * N * k + i] = lo;
+            dwl[2 * N * k + N + i] = hi;
+            if (leaf && k == 0) std::memcpy(&dt[8 * (size_t)leaf_slot[i] + 3].z, &hb, 4);
+        }
     }
     drop_graph(c);
     free_scene(c);
@@ -1563,7 +1602,8 @@ int pt_upload_scene(pt_ctx* c, const float* tris, int n_tris, const float* bvh, 
     c->n_mats = n_mats;
     c->n_slots = 2 * n_leaves;
     // exact-reciprocal slab guard, scene half: every box coordinate is 0
-    // or has magnitude in [2^-40, 2^60]
+    // or has magnitude in [2^-40, 2^60], and min <= max on every axis (the octant images'
+    // near-first order, slab_oct)
     c->scene_fast = 1;
     for (int i = 0; i < n_nodes && c->scene_fast; i++) {
         const float* nd = bvh + 12 * (size_t)i;
@@ -1572,8 +1612,9 @@ int pt_upload_scene(pt_ctx* c, const float* tris, int n_tris, const float* bvh, 
             float a = std::fabs(nd[q]);
             if (!(nd[q] == 0.0f || (a >= 0x1p-40f && a <= 0x1p60f))) { c->scene_fast = 0; break; }
         }
+        if (!(nd[0] <= nd[4] && nd[1] <= nd[5] && nd[2] <= nd[6])) c->scene_fast = 0;
     }
-    c->lds_bytes = (size_t)(2 * n_nodes + 4 * c->n_slots + 3 * n_mats + 2 * n_spheres) * sizeof(float4);
+    c->lds_bytes = (size_t)(16 * n_nodes + 4 * c->n_slots + 3 * n_mats + 2 * n_spheres) * sizeof(float4);
     c->root_child = -1;
     if (n_nodes > 0) {
         const float4 r0 = dn[0], r1 = dn[1];
