@@ -159,6 +159,70 @@ PT_HD float cosf_pinned(float xx) {
     return neg ? -r : r;
 }
 
+// Branch-free forms of logf_pinned / cosf_pinned for the kernels' Box-Muller draw: the same
+// operations on the same values, every fdlibm / Cephes branch evaluated and chosen by a
+// select (a wave otherwise runs each divergent branch in turn, with exec-mask bookkeeping).
+// Bit-identical to the branchy forms over their whole hot-path domains (x in {0} U
+// [2^-32, 1] for log, every finite theta in [0, 2*pi] for cos): checked exhaustively on the
+// host (tests/test_exact_div.py) and on the GPU (tools/verify_fastmath.hip).
+//   log: fdlibm's k == 0 returns are the general k != 0 expressions with dk = +0 (RN(a - b)
+//   = -RN(b - a), x - 0 = x, and 0 - (+-0) = +0 = f - f), so only the small-|f| / main and
+//   ii > 0 choices remain; f == 0 (x a power of two) is the small-|f| expression at f = 0.
+PT_HD float logf_bf(float x) {                     // x in {0} U [2^-32, 1]
+    const float ln2_hi = 6.9313812256e-01f, ln2_lo = 9.0580006145e-06f;
+    const float Lg1 = bitsf(0x3f2aaaaau), Lg2 = bitsf(0x3ecccce1u), Lg3 = bitsf(0x3e91e9eeu),
+                Lg4 = bitsf(0x3e789e26u);
+    int32_t ix = (int32_t)fbits(x);
+    int32_t k = (ix >> 23) - 127;
+    ix &= 0x007fffff;
+    const int32_t i = (ix + (0x95f64 << 3)) & 0x800000;
+    const float xr = bitsf((uint32_t)(ix | (i ^ 0x3f800000)));
+    k += (i >> 23);
+    const float f = xr - 1.0f;
+    const float dk = (float)k;
+    const float hi = dk * ln2_hi, lo = dk * ln2_lo;
+    // |f| < 2^-20 branch
+    const float Rs = f * f * (0.5f - 0.33333333333333333f * f);
+    const float small = hi - ((Rs - lo) - f);
+    // main branch (2 + f in [1.58, 2.42]: exact reciprocal + Markstein, as logf_pinned)
+    const float tf = 2.0f + f;
+    const float s = div_mk(f, tf, rcp_fast(tf));
+    const float z = s * s;
+    const float w = z * z;
+    const float t1 = w * (Lg2 + w * Lg4);
+    const float t2 = z * (Lg1 + w * Lg3);
+    const float R = t2 + t1;
+    const int32_t ii = (ix - (0x6147a << 3)) | ((0x6b851 << 3) - ix);
+    const float hfsq = 0.5f * f * f;
+    const float m1 = hi - ((hfsq - (s * (hfsq + R) + lo)) - f);
+    const float m2 = hi - ((s * (f - R) - lo) - f);
+    float r = ii > 0 ? m1 : m2;
+    r = ((0x007fffff & (0x8000 + ix)) < 0xc000) ? small : r;
+    return x == 0.0f ? bitsf(0xff800000u) : r;
+}
+PT_HD float cosf_bf(float xx) {                    // finite xx >= 0 (theta in [0, 2*pi])
+    const float DP1 = 0.78515625f, DP2 = 2.4187564849853515625e-4f, DP3 = 3.77489497744594108e-8f,
+                FOPI = 1.27323954473516f;
+    const float x0 = bitsf(fbits(xx) & 0x7fffffffu);
+    int j = (int)(FOPI * x0);
+    float y = (float)j;
+    const bool odd = (j & 1) != 0;
+    j = odd ? j + 1 : j;
+    y = odd ? y + 1.0f : y;
+    j &= 7;
+    bool neg = j > 3;
+    j = j > 3 ? j - 4 : j;
+    neg = (j > 1) != neg;
+    const float x = ((x0 - y * DP1) - y * DP2) - y * DP3;
+    const float z = x * x;
+    const float rs = ((-1.9515295891E-4f * z + 8.3321608736E-3f) * z - 1.6666654611E-1f) * z * x + x;
+    float rc = ((2.443315711809948E-005f * z - 1.388731625493765E-003f) * z + 4.166664568298827E-002f) * z * z;
+    rc -= 0.5f * z;
+    rc += 1.0f;
+    const float r = (j == 1 || j == 2) ? rs : rc;
+    return neg ? -r : r;
+}
+
 struct f3 { float x, y, z; };
 PT_HD f3 mk(float x, float y, float z) { f3 r; r.x = x; r.y = y; r.z = z; return r; }
 PT_HD f3 operator+(f3 a, f3 b) { return mk(a.x + b.x, a.y + b.y, a.z + b.z); }
@@ -203,8 +267,13 @@ PT_HD float random_normal(uint32_t& s) {            // :115-120 (theta first, th
     return __builtin_sqrtf(-1.3862944f * __builtin_amdgcn_logf(u2)) * __builtin_amdgcn_cosf(u1);
 #endif
     float theta = (2.0f * 3.1415926f) * random01(s);
+#if defined(__HIP_DEVICE_COMPILE__)
+    float rho = sqrt_g(-2.0f * logf_bf(random01(s)));
+    return rho * cosf_bf(theta);
+#else
     float rho = sqrt_g(-2.0f * logf_pinned(random01(s)));
     return rho * cosf_pinned(theta);
+#endif
 }
 PT_HD f3 random_unit_vector(uint32_t& s) {          // :122-129, x, y, z order
     float x = random_normal(s);

@@ -3,7 +3,10 @@ q0 = a*rd; r = fma(-q0, d, a); q = fma(r, rd, q0) with rd = RN(1/d) equals RN(a/
 bit (Markstein's theorem).  Checked here on the host with IEEE fmaf over 2e7 random pairs
 spanning the guarded ranges plus structured near-tie cases; the GPU kernels use the same
 v_fma_f32 sequence and are checked image-wise by tests/test_gpu_parity.py."""
+import os
 import subprocess
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 PROG = r"""
 #include <math.h>
@@ -99,3 +102,17 @@ def test_markstein_quotient_is_correctly_rounded(tmp_path):
     out = subprocess.run([str(exe), "20000000"], capture_output=True, text=True)
     assert out.returncode == 0, out.stdout
     assert "bad=0" in out.stdout
+
+
+def test_branch_free_box_muller_forms(tmp_path):
+    """The kernels' branch-free logf_bf / cosf_bf (pt_math.h) return the same bits as the
+    branchy fdlibm logf / Cephes cosf restatements: every 7th binary32 of the hot-path
+    domains here (tools/verify_bf.cpp; stride 1 runs the exhaustive check in ~40 s, and
+    tools/verify_fastmath.hip checks every input on the GPU)."""
+    exe = tmp_path / "verify_bf"
+    subprocess.check_call(["g++", "-O2", "-std=c++17", "-ffp-contract=off", "-march=x86-64-v3", "-pthread",
+                           os.path.join(REPO, "tools", "verify_bf.cpp"), "-o", str(exe)])
+    out = subprocess.run([str(exe), "7"], capture_output=True, text=True, timeout=300)
+    assert out.returncode == 0, out.stdout
+    lines = [l for l in out.stdout.splitlines() if "tested=" in l]
+    assert len(lines) == 2 and all(" bad=0" in l for l in lines), out.stdout

@@ -2,8 +2,9 @@
 sqrt_fast): bit-identical to the correctly rounded 1.0f/x and sqrtf(x) for every binary32
 in the guarded range [2^-100, 2^100] (both signs for the reciprocal), on this GPU's
 v_rcp_f32 / v_sqrt_f32; and logf_pinned's quotient f/(2+f) by an exact reciprocal plus a
-Markstein correction, for every |f| in [2^-21, 0.5].  The kernels use these forms only
-inside those ranges."""
+Markstein correction, for every |f| in [2^-21, 0.5]; and the branch-free Box-Muller forms
+logf_bf / cosf_bf against the branchy fdlibm / Cephes restatements on their whole domains.
+The kernels use these forms only inside those ranges."""
 import os
 import subprocess
 
@@ -22,7 +23,7 @@ def test_fast_rcp_sqrt_exhaustive(tmp_path):
     out = subprocess.run([exe], capture_output=True, text=True, timeout=600)
     print(out.stdout)
     lines = [l for l in out.stdout.splitlines() if "tested=" in l]
-    assert len(lines) == 5, out.stdout + out.stderr
+    assert len(lines) == 7, out.stdout + out.stderr
     for l in lines:
         assert " bad=0 " in l, l
     assert out.returncode == 0
