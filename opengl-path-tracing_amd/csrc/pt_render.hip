@@ -1347,8 +1347,8 @@ struct pt_ctx {
     int root_child = -1;
     size_t lds_bytes = 0;
     unsigned persist_blocks = 2048;
-    // 0 = automatic: 32/48 when the scene is staged in LDS (best on C2), 16/32 when the walk
-    // reads global memory (latency-bound; best on the C3 stand-in) -- tools/probe.py sweeps
+    // 0 = automatic: 52/44 when the scene is staged in LDS (best on C2 since the octant walk),
+    // 16/32 when the walk reads global memory (best on the C3 stand-in) -- tools/probe.py sweeps
     int leaf_thresh = 0, shade_thresh = 0, minw = 0;
     // frame-split work items (KParams::group): 0 = automatic, n = frames per item
     int group_force = 0;
@@ -1760,8 +1760,8 @@ static int enqueue_render(pt_ctx* c, int frame_first, int n_frames, int acc_firs
     p.root_child = c->root_child;
     {
         bool lds_scene = c->lds_bytes <= kLdsSceneMax && c->variant != 3;
-        p.leaf_thresh = c->leaf_thresh ? c->leaf_thresh : (lds_scene ? 32 : 16);
-        p.shade_thresh = c->shade_thresh ? c->shade_thresh : (lds_scene ? 48 : 32);
+        p.leaf_thresh = c->leaf_thresh ? c->leaf_thresh : (lds_scene ? 52 : 16);
+        p.shade_thresh = c->shade_thresh ? c->shade_thresh : (lds_scene ? 44 : 32);
     }
     p.rW = 1.0f / (float)p.W;
     p.rH = 1.0f / (float)p.H;
