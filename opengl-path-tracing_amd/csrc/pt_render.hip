@@ -54,6 +54,7 @@ struct KParams {
     unsigned long long* counters;  // [5] when counting
     unsigned int* work_counter;    // persistent kernel pixel queue
     int n_slots, n_mats;           // triangle slots / materials (LDS staging sizes)
+    int n_top;                     // global-memory scene: nodes [0, n_top) staged in LDS
     int scene_fast;                // every box coordinate inside the exact-reciprocal guard
     int leaf_thresh, shade_thresh; // wave scheduling thresholds of the state-machine kernel
     const int* frame_dev;          // progressive graph: device frame counter (null = use frame_first)
@@ -430,6 +431,11 @@ __device__ __forceinline__ void node_at(const SceneView& S, int i, float4& lo, f
     if (LDS) {      // i = byte offset from the LDS base, which is 0 (checked at kernel entry)
         const v4f x = *(lds_v4f*)(size_t)(unsigned)i;
         const v4f y = *(lds_v4f*)(size_t)(unsigned)(i + (S.np << 4));
+        lo = make_float4(x.x, x.y, x.z, x.w);
+        hi = make_float4(y.x, y.y, y.z, y.w);
+    } else if (i < S.np) {   // global-memory scene: a top node, staged in LDS
+        const v4f x = *(lds_v4f*)(size_t)(unsigned)(i << 4);
+        const v4f y = *(lds_v4f*)(size_t)(unsigned)((i + S.np) << 4);
         lo = make_float4(x.x, x.y, x.z, x.w);
         hi = make_float4(y.x, y.y, y.z, y.w);
     } else {
@@ -961,7 +967,13 @@ __global__ __launch_bounds__(256, MINW) void k_render_sm(KParams p) {
         S.tris = p.sc.tris;
         S.mats = p.sc.mats;
         S.spheres = p.sc.spheres;
-        S.np = S.tp = 0;
+        // the top nodes (breadth-first numbering) in LDS planes: lo at [i], hi at [n_top + i]
+        if ((unsigned)(size_t)(__attribute__((address_space(3))) const char*)g_lds != 0u) __builtin_trap();
+        const int K = p.n_top;
+        for (int i = threadIdx.x; i < 2 * K; i += blockDim.x) lds[(i & 1) * K + (i >> 1)] = p.sc.nodes[i];
+        __syncthreads();
+        S.np = K;
+        S.tp = 0;
     }
     const int lane = threadIdx.x & 63;
     const f3 cpos = mk(p.cam[0], p.cam[1], p.cam[2]), cfwd = mk(p.cam[3], p.cam[4], p.cam[5]);
@@ -1317,6 +1329,9 @@ __global__ __launch_bounds__(256) void k_aces(const float4* __restrict__ src, uc
 
 // ===================================================================== host side
 constexpr size_t kLdsSceneMax = 48 * 1024;   // stage the scene in LDS up to 48 KiB
+// global-memory scenes: the first kTopNodes device nodes (breadth-first from the root) are
+// staged in LDS, 24 KiB per workgroup (6 workgroups per CU stay resident)
+constexpr int kTopNodes = 768;
 
 struct pt_ctx {
     pt_config cfg{};
@@ -1342,7 +1357,7 @@ struct pt_ctx {
     hipGraph_t graph = nullptr;
     hipGraphExec_t graph_exec = nullptr;
     int graph_frames = 0;
-    int n_nodes = 0, n_spheres = 0, n_mats = 0, n_slots = 0, scene_fast = 0;
+    int n_nodes = 0, n_spheres = 0, n_mats = 0, n_slots = 0, scene_fast = 0, n_top = 0;
     float root_box[6] = {0, 0, 0, 0, 0, 0};
     int root_child = -1;
     size_t lds_bytes = 0;
@@ -1507,6 +1522,26 @@ int pt_upload_scene(pt_ctx* c, const float* tris, int n_tris, const float* bvh, 
         int m = (int)spheres[8 * (size_t)i + 4];
         if (m < 0 || m >= n_mats) return fail(c, PT_E_SCENE, "sphere material index out of range");
     }
+    // --- device node numbering: the first kTopNodes nodes in breadth-first order of the walk
+    // links from the root (the nodes nearly every walk passes: the global-memory walk keeps
+    // them in LDS, node_at), the rest in their original order.  Links are renumbered with the
+    // nodes, so every walk visits the same node sequence; the root stays node 0.
+    std::vector<int> pos(n_nodes, -1);
+    {
+        int nx = 0;
+        std::vector<int> q;
+        if (n_nodes > 0) { pos[0] = nx++; q.push_back(0); }
+        for (size_t qi = 0; qi < q.size() && nx < kTopNodes; qi++) {
+            const float* nd = bvh + 12 * (size_t)q[qi];
+            for (int l = 10; l < 12; l++) {
+                const int t = (int)nd[l];
+                if (t >= 0 && pos[t] < 0 && nx < kTopNodes) { pos[t] = nx++; q.push_back(t); }
+            }
+        }
+        for (int i = 0; i < n_nodes; i++)
+            if (pos[i] < 0) pos[i] = nx++;
+    }
+    std::vector<int> slot_of(n_nodes, -1);   // leaf slot by device node index
     // --- transpose to device layouts
     std::vector<float4> dt(8 * (size_t)std::max(n_leaves, 1));
     auto put_tri = [&](float4* q, int ti) {
@@ -1532,16 +1567,19 @@ int pt_upload_scene(pt_ctx* c, const float* tris, int n_tris, const float* bvh, 
             put_tri(&dt[8 * (size_t)s + 4], t1);
             a = ~((s << 1) | (t0 == t1 ? 1 : 0));
             b = (int)nd[11];
+            slot_of[pos[i]] = s;
         } else {
-            a = (int)nd[10];
+            a = pos[(int)nd[10]];
             b = (int)nd[11];
         }
+        if (b >= 0) b = pos[b];
         float fa, fb;
         std::memcpy(&fa, &a, 4);
         std::memcpy(&fb, &b, 4);
         // axis-paired: (min, max) of one axis in adjacent registers for packed-f32 slabs
-        dn[2 * (size_t)i] = make_float4(nd[0], nd[4], nd[1], nd[5]);
-        dn[2 * (size_t)i + 1] = make_float4(nd[2], nd[6], fa, fb);
+        const size_t j = (size_t)pos[i];
+        dn[2 * j] = make_float4(nd[0], nd[4], nd[1], nd[5]);
+        dn[2 * j + 1] = make_float4(nd[2], nd[6], fa, fb);
     }
     std::vector<float4> dm(3 * (size_t)std::max(n_mats, 1));
     for (int i = 0; i < n_mats; i++) {
@@ -1582,7 +1620,7 @@ int pt_upload_scene(pt_ctx* c, const float* tris, int n_tris, const float* bvh, 
             if (k & 4) std::swap(hi.x, hi.y);
             dwl[2 * N * k + i] = lo;
             dwl[2 * N * k + N + i] = hi;
-            if (leaf && k == 0) std::memcpy(&dt[8 * (size_t)leaf_slot[i] + 3].z, &hb, 4);
+            if (leaf && k == 0) std::memcpy(&dt[8 * (size_t)slot_of[i] + 3].z, &hb, 4);
         }
     }
     drop_graph(c);
@@ -1601,6 +1639,7 @@ int pt_upload_scene(pt_ctx* c, const float* tris, int n_tris, const float* bvh, 
     c->n_spheres = n_spheres;
     c->n_mats = n_mats;
     c->n_slots = 2 * n_leaves;
+    c->n_top = std::min(n_nodes, kTopNodes);
     // exact-reciprocal slab guard, scene half: every box coordinate is 0
     // or has magnitude in [2^-40, 2^60], and min <= max on every axis (the octant images'
     // near-first order, slab_oct)
@@ -1754,6 +1793,7 @@ static int enqueue_render(pt_ctx* c, int frame_first, int n_frames, int acc_firs
     p.counters = c->d_counters;
     p.work_counter = c->d_work;
     p.n_slots = c->n_slots;
+    p.n_top = c->n_top;
     p.n_mats = c->n_mats;
     p.scene_fast = c->scene_fast;
     std::memcpy(p.root_box, c->root_box, sizeof(p.root_box));
@@ -1813,13 +1853,14 @@ static int enqueue_render(pt_ctx* c, int frame_first, int n_frames, int acc_firs
         // occupancy: 6 waves/SIMD (80 VGPRs) measured best for LDS scenes (+5% on C2 over 5),
         // a tie for global-memory scenes
         const int mw = c->minw ? c->minw : 6;
+        const size_t top_lds = (size_t)c->n_top * 2 * sizeof(float4);   // global scene: top nodes
 #define PT_LAUNCH_SM(L, M)                                                                                    \
-    if (c->counting && p.rgb) hipLaunchKernelGGL((k_render_sm<true, L, 5, M, true>), grid, dim3(256), L ? lds : 0, c->stream, p); \
-    else if (c->counting) hipLaunchKernelGGL((k_render_sm<true, L, 5, M, false>), grid, dim3(256), L ? lds : 0, c->stream, p); \
-    else if (p.rgb && mw == 6) hipLaunchKernelGGL((k_render_sm<false, L, 6, M, true>), grid, dim3(256), L ? lds : 0, c->stream, p); \
-    else if (p.rgb) hipLaunchKernelGGL((k_render_sm<false, L, 5, M, true>), grid, dim3(256), L ? lds : 0, c->stream, p); \
-    else if (mw == 6) hipLaunchKernelGGL((k_render_sm<false, L, 6, M, false>), grid, dim3(256), L ? lds : 0, c->stream, p); \
-    else hipLaunchKernelGGL((k_render_sm<false, L, 5, M, false>), grid, dim3(256), L ? lds : 0, c->stream, p);
+    if (c->counting && p.rgb) hipLaunchKernelGGL((k_render_sm<true, L, 5, M, true>), grid, dim3(256), L ? lds : top_lds, c->stream, p); \
+    else if (c->counting) hipLaunchKernelGGL((k_render_sm<true, L, 5, M, false>), grid, dim3(256), L ? lds : top_lds, c->stream, p); \
+    else if (p.rgb && mw == 6) hipLaunchKernelGGL((k_render_sm<false, L, 6, M, true>), grid, dim3(256), L ? lds : top_lds, c->stream, p); \
+    else if (p.rgb) hipLaunchKernelGGL((k_render_sm<false, L, 5, M, true>), grid, dim3(256), L ? lds : top_lds, c->stream, p); \
+    else if (mw == 6) hipLaunchKernelGGL((k_render_sm<false, L, 6, M, false>), grid, dim3(256), L ? lds : top_lds, c->stream, p); \
+    else hipLaunchKernelGGL((k_render_sm<false, L, 5, M, false>), grid, dim3(256), L ? lds : top_lds, c->stream, p);
         if (c->variant == 0 || c->variant == 3) {
             bool multi = p.rpp > 1;
             if (use_lds && multi) { PT_LAUNCH_SM(true, true) }
