@@ -605,6 +605,94 @@ __device__ __forceinline__ float tri_hit_lazy(const SceneView& S, int slot, floa
     return ok ? t : -1.0f;
 }
 
+// hit_triangle split in two for the leaf phase's edge-test compaction: the plane distance
+// (:285-297) and the three edge tests at that distance (:299-306), the same operations as
+// tri_hit_bf in the same order, so the same bits.
+template <bool LDS>
+__device__ __forceinline__ float tri_plane(const SceneView& S, int slot, float4 q3, f3 o, f3 d) {
+    const f3 n = mk(tri_quad<LDS>(S, slot, 0).w, tri_quad<LDS>(S, slot, 1).w, tri_quad<LDS>(S, slot, 2).w);
+    return -(pt::dot(n, o) + q3.x) / pt::dot(n, d);
+}
+template <bool LDS>
+__device__ __forceinline__ bool tri_edges(const SceneView& S, int slot, f3 o, f3 d, float t) {
+    const float4 q0 = tri_quad<LDS>(S, slot, 0), q1 = tri_quad<LDS>(S, slot, 1), q2 = tri_quad<LDS>(S, slot, 2);
+    const f3 n = mk(q0.w, q1.w, q2.w);
+    const f3 v0 = mk(q0.x, q0.y, q0.z), v1 = mk(q1.x, q1.y, q1.z), v2 = mk(q2.x, q2.y, q2.z);
+    const f3 p = o + d * t;
+    const float e0 = pt::dot(n, pt::cross(v1 - v0, p - v0));
+    const float e1 = pt::dot(n, pt::cross(v2 - v1, p - v1));
+    const float e2 = pt::dot(n, pt::cross(v0 - v2, p - v2));
+    return (e0 > 0.0f) && (e1 > 0.0f) && (e2 > 0.0f);
+}
+template <bool LDS>
+__device__ __forceinline__ bool tri_edges_at(const SceneView& S, int slot, f3 p) {
+    const float4 q0 = tri_quad<LDS>(S, slot, 0), q1 = tri_quad<LDS>(S, slot, 1), q2 = tri_quad<LDS>(S, slot, 2);
+    const f3 n = mk(q0.w, q1.w, q2.w);
+    const f3 v0 = mk(q0.x, q0.y, q0.z), v1 = mk(q1.x, q1.y, q1.z), v2 = mk(q2.x, q2.y, q2.z);
+    const float e0 = pt::dot(n, pt::cross(v1 - v0, p - v0));
+    const float e1 = pt::dot(n, pt::cross(v2 - v1, p - v1));
+    const float e2 = pt::dot(n, pt::cross(v0 - v2, p - v2));
+    return (e0 > 0.0f) && (e1 > 0.0f) && (e2 > 0.0f);
+}
+__device__ __forceinline__ float fperm_f(int dst_bytes, float v) {
+    return __int_as_float(__builtin_amdgcn_ds_permute(dst_bytes, __float_as_int(v)));
+}
+
+// The leaf phase of calculateRayCollision (:406-429) for the lanes at a leaf (`at`), with the
+// edge tests compacted over the wave.  A leaf's 2-way choice
+//   c1 = h1 > 1e-4 && h1 < t && (h1 < h2 || h2 < 1e-4),  c2 = !c1 && h2 > 1e-4 && h2 < t
+// only depends on a triangle's edge verdict when its plane distance lies in (1e-4, t) for the
+// first triangle and in [1e-4, t) for the second (outside those ranges both verdicts give the
+// same c1 / c2: h1 <= 1e-4 fails c1 either way; h2 < 1e-4 or a miss (-1) both satisfy
+// `h2 < 1e-4` and fail c2).  About 47% of the triangle tests of a Cornell frame need them
+// (81% with the plain t >= 0 cull: a bounce ray starts ON the surface it left, at a plane
+// distance near 0).  The wave's needed (lane, triangle) pairs are packed onto its first lanes
+// -- a forward permute hands each worker lane its source, backward permutes fetch o, d and
+// the plane distance -- so one pass of edge tests serves both triangles of every lane; a
+// ballot returns the verdicts.  More than 63 pairs: each lane tests its own.  Every edge
+// test runs the same operations on the same values as at its source lane: the same bits.
+// Returns (through h1 / h2) the hit_triangle results up to that equivalence.
+template <bool LDS>
+__device__ __forceinline__ void leaf_pair_tests(const SceneView& S, bool at, int s0, float4 q3a, float4 q3b,
+                                                f3 o, f3 d, float t, int lane, float& h1, float& h2) {
+    float ta = 0.0f, tb = 0.0f;
+    if (at) {
+        ta = tri_plane<LDS>(S, s0, q3a, o, d);
+        tb = tri_plane<LDS>(S, s0 + 1, q3b, o, d);
+    }
+    const bool na = at && ta > 0.0001f && ta < t;
+    const bool nb = at && tb >= 0.0001f && tb < t;
+    const unsigned long long ma = __ballot(na), mb = __ballot(nb);
+    const int ca = __popcll(ma), n = ca + __popcll(mb);
+    bool oka = false, okb = false;
+    if (n <= 63) {
+        const unsigned long long below = (1ull << lane) - 1ull;
+        const int ja = __popcll(ma & below), jb = ca + __popcll(mb & below);
+        // forward permutes hand worker j its pair's hit point o + d*t and slot; lanes
+        // without a pair send to lane 63, never a worker (n <= 63)
+        const int da = (na ? ja : 63) << 2, db = (nb ? jb : 63) << 2;
+        const f3 pa = o + d * ta, pb = o + d * tb;
+        const bool first = lane < ca;
+        // (all eight permutes run on the full wave: a permute only moves data between
+        // active lanes, so none of them may sit under the `first` select)
+        const float ax = fperm_f(da, pa.x), ay = fperm_f(da, pa.y), az = fperm_f(da, pa.z);
+        const float bx = fperm_f(db, pb.x), by = fperm_f(db, pb.y), bz = fperm_f(db, pb.z);
+        const int as = __builtin_amdgcn_ds_permute(da, s0), bs = __builtin_amdgcn_ds_permute(db, s0 + 1);
+        const f3 wp = first ? mk(ax, ay, az) : mk(bx, by, bz);
+        const int ws = first ? as : bs;
+        bool pass = false;
+        if (lane < n) pass = tri_edges_at<LDS>(S, ws, wp);
+        const unsigned long long r = __ballot(pass);
+        oka = na && ((r >> ja) & 1ull);
+        okb = nb && ((r >> jb) & 1ull);
+    } else {
+        if (na) oka = tri_edges<LDS>(S, s0, o, d, ta);
+        if (nb) okb = tri_edges<LDS>(S, s0 + 1, o, d, tb);
+    }
+    h1 = oka ? ta : -1.0f;
+    h2 = okb ? tb : -1.0f;
+}
+
 // calculateRayCollision with "while-while" scheduling of the stackless walk: each lane
 // advances through the link chain until it reaches a leaf whose box it hits (or the walk
 // ends), and only then do the lanes that stopped at leaves run the two triangle tests
@@ -871,6 +959,9 @@ __global__ __launch_bounds__(256, MINW) void k_render_wave(KParams p) {
 // =====================================================================================
 enum : int { ST_DONE = 0, ST_TRAV = 1, ST_LEAF = 2, ST_SHADE = 3 };
 constexpr unsigned kPullBatch = 32;
+#ifndef PT_LEAF_COMPACT
+#define PT_LEAF_COMPACT 1   // leaf phase: edge tests compacted over the wave (leaf_pair_tests)
+#endif
 constexpr int kWalkUnroll = 4;   // node steps per yield check of the walk (measured: 1 -> 2 +3.6%, 4 +5.7%, 6/8 slower)
 
 // The TRAV phase: each TRAV lane advances one node per iteration (bvh_intersect + the link
@@ -1235,23 +1326,36 @@ __global__ __launch_bounds__(256, MINW) void k_render_sm(KParams p) {
             }
         } else if (nL > 0 && (nL >= p.leaf_thresh || nT == 0)) {
             // ---------------- LEAF: both triangle tests + the 2-way choice (:406-429)
-            if (st == ST_LEAF) {
+            const bool at = st == ST_LEAF;
+            int s0 = 0, cont = -1;
+            float4 q3 = make_float4(0, 0, 0, 0);
+            if (at) {
                 if (COUNT) { c.tri += 2; diag_tick(c.lw, c.ll); }
                 const int code = LDS ? leaf : ~leaf;         // (slot << 1) | single
-                const int s0 = code & ~1;                    // slots 2k, 2k+1
-                const float4 q3 = tri_quad<LDS>(S, s0, 3);   // .z / .w: the leaf's next-right
-                int cont = LDS ? __float_as_int(q3.z) : bi;      // LDS: offset in image 0
+                s0 = code & ~1;                              // slots 2k, 2k+1
+                q3 = tri_quad<LDS>(S, s0, 3);                // .z / .w: the leaf's next-right
+                cont = LDS ? __float_as_int(q3.z) : bi;      // LDS: offset in image 0
                 if (LDS && fast && cont >= 0) cont += oct_base(d, S.np << 5);
-                f3 n0, n1;
-                float h1, h2;
-                if (p.flags & PT_FLAG_MOLLER_TRUMBORE) {   // wave-uniform
+            }
+            float h1 = -1.0f, h2 = -1.0f;
+            if (p.flags & PT_FLAG_MOLLER_TRUMBORE) {   // wave-uniform
+                if (at) {
                     h1 = tri_mt(tri_quad<LDS>(S, s0, 0), tri_quad<LDS>(S, s0, 1), tri_quad<LDS>(S, s0, 2), o, d);
                     h2 = tri_mt(tri_quad<LDS>(S, s0 + 1, 0), tri_quad<LDS>(S, s0 + 1, 1),
                                 tri_quad<LDS>(S, s0 + 1, 2), o, d);
-                } else {
+                }
+            } else {
+#if PT_LEAF_COMPACT
+                leaf_pair_tests<LDS>(S, at, s0, q3, at ? tri_quad<LDS>(S, s0 + 1, 3) : q3, o, d, t, lane, h1, h2);
+#else
+                if (at) {
+                    f3 n0, n1;
                     h1 = tri_hit_lazy<LDS>(S, s0, q3, o, d, t, n0);
                     h2 = tri_hit_lazy<LDS>(S, s0 + 1, tri_quad<LDS>(S, s0 + 1, 3), o, d, t, n1);
                 }
+#endif
+            }
+            if (at) {
                 bool c1 = h1 > 0.0001f && h1 < t && (h1 < h2 || h2 < 0.0001f);
                 bool c2 = !c1 && h2 > 0.0001f && h2 < t;
                 if (c1 || c2) {
