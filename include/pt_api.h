@@ -132,6 +132,8 @@ int pt_set_kernel(pt_ctx* ctx, int variant);
  * key 5 = frames per work item (>= 1; 0 = auto, 2..8): a pixel's frames are spread over
  *         several lanes and the running mean is applied by a second kernel in frame order;
  *         a value >= n_frames gives each lane whole pixels (running mean in registers).
+ * key 6 = walk floor (1..64, 0 = auto): a walk phase ends once fewer lanes than this still
+ *         walk, and the leaf (or shading) phase runs even below its threshold.
  * None of these change the image (each pixel's frames stay in order in one lane). */
 int pt_set_tuning(pt_ctx* ctx, int key, int value);
 

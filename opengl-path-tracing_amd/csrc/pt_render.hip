@@ -57,6 +57,7 @@ struct KParams {
     int n_top;                     // global-memory scene: nodes [0, n_top) staged in LDS
     int scene_fast;                // every box coordinate inside the exact-reciprocal guard
     int leaf_thresh, shade_thresh; // wave scheduling thresholds of the state-machine kernel
+    int trav_floor;                // ... and the walk floor: fewer walking lanes end a walk phase
     const int* frame_dev;          // progressive graph: device frame counter (null = use frame_first)
     int frame_offset;              // this launch's frame offset from *frame_dev
     const unsigned* tile_perm;     // queue order of 8x8 tiles (null = raster order)
@@ -977,7 +978,7 @@ constexpr int kWalkUnroll = 4;   // node steps per yield check of the walk (meas
 template <bool ALL_FAST, bool COUNT, bool LDS>
 __device__ __forceinline__ void trav_walk(const SceneView& S, f3 o, f3 d, f3 rd, bool fast, float t,
                                           unsigned long long live, int leaf_thresh, int shade_thresh,
-                                          int& st, int& bi, int& leaf, Cnt& c) {
+                                          int trav_floor, int& st, int& bi, int& leaf, Cnt& c) {
     const int min_thresh = leaf_thresh < shade_thresh ? leaf_thresh : shade_thresh;
     // Inside the walk one register carries the lane's state (WalkLinks): w >= 0 the next
     // node, w == -1 the chain ended (-> SHADE), w <= -2 stopped at the hit leaf with code
@@ -1010,6 +1011,7 @@ __device__ __forceinline__ void trav_walk(const SceneView& S, f3 o, f3 d, f3 rd,
         for (int u = 0; u < kWalkUnroll; u++) step();
         unsigned long long mt = __ballot(w >= 0);
         if (!mt) break;
+        if (__popcll(mt) < trav_floor) break;     // too few walkers: run a waiting phase
         if (__popcll(live & ~mt) >= min_thresh) {
             if (__popcll(pre_leaf | __ballot(w <= -2)) >= leaf_thresh) break;
             if (__popcll(pre_shade | (__ballot(w == -1) & mw)) >= shade_thresh) break;
@@ -1111,10 +1113,14 @@ __global__ __launch_bounds__(256, MINW) void k_render_sm(KParams p) {
 #ifdef PT_PHASE_CLOCK
         const unsigned long long clk_t0 = clock64();
         int clk_ph = 2;
-        if (nS > 0 && (nS >= p.shade_thresh || (nT == 0 && nL == 0))) clk_ph = 0;
-        else if (nL > 0 && (nL >= p.leaf_thresh || nT == 0)) clk_ph = 1;
+        if (nS > 0 && (nS >= p.shade_thresh || (nT < p.trav_floor && nL == 0))) clk_ph = 0;
+        else if (nL > 0 && (nL >= p.leaf_thresh || nT < p.trav_floor)) clk_ph = 1;
 #endif
-        if (nS > 0 && (nS >= p.shade_thresh || (nT == 0 && nL == 0))) {
+        // phase choice: SHADE / LEAF once their thresholds are reached, otherwise TRAV while
+        // at least trav_floor lanes walk; below the floor the leaf phase runs if any lane
+        // waits at a leaf, else shading (trav_floor 1 = walk until no lane walks)
+        const bool low = nT < p.trav_floor;
+        if (nS > 0 && (nS >= p.shade_thresh || (low && nL == 0))) {
             // ---------------- SHADE: finish segment, regenerate, set up next segment
             if (st == ST_SHADE && !fresh) {
                 const bool hit = hprim != -1;
@@ -1324,7 +1330,7 @@ __global__ __launch_bounds__(256, MINW) void k_render_sm(KParams p) {
                 bi = walk ? (inside ? root_skip : 0) + img : -1;
                 st = walk ? ST_TRAV : ST_SHADE;
             }
-        } else if (nL > 0 && (nL >= p.leaf_thresh || nT == 0)) {
+        } else if (nL > 0 && (nL >= p.leaf_thresh || low)) {
             // ---------------- LEAF: both triangle tests + the 2-way choice (:406-429)
             const bool at = st == ST_LEAF;
             int s0 = 0, cont = -1;
@@ -1372,9 +1378,9 @@ __global__ __launch_bounds__(256, MINW) void k_render_sm(KParams p) {
             // the per-node IEEE-division branch.
             const unsigned long long live = __ballot(st != ST_DONE);
             if (__all(fast || st != ST_TRAV))
-                trav_walk<true, COUNT, LDS>(S, o, d, rd, fast, t, live, p.leaf_thresh, p.shade_thresh, st, bi, leaf, c);
+                trav_walk<true, COUNT, LDS>(S, o, d, rd, fast, t, live, p.leaf_thresh, p.shade_thresh, p.trav_floor, st, bi, leaf, c);
             else
-                trav_walk<false, COUNT, LDS>(S, o, d, rd, fast, t, live, p.leaf_thresh, p.shade_thresh, st, bi, leaf, c);
+                trav_walk<false, COUNT, LDS>(S, o, d, rd, fast, t, live, p.leaf_thresh, p.shade_thresh, p.trav_floor, st, bi, leaf, c);
         }
 #ifdef PT_PHASE_CLOCK
         clk[clk_ph] += clock64() - clk_t0;
@@ -1467,8 +1473,9 @@ struct pt_ctx {
     size_t lds_bytes = 0;
     unsigned persist_blocks = 2048;
     // 0 = automatic: 52/44 when the scene is staged in LDS (best on C2 since the octant walk),
-    // 16/32 when the walk reads global memory (best on the C3 stand-in) -- tools/probe.py sweeps
-    int leaf_thresh = 0, shade_thresh = 0, minw = 0;
+    // 16/32 when the walk reads global memory (best on the C3 stand-in); walk floor 8 / 6
+    // (+0.8% on C2, +0.5% on C3 over no floor) -- tools/probe.py sweeps
+    int leaf_thresh = 0, shade_thresh = 0, minw = 0, trav_floor = 0;
     // frame-split work items (KParams::group): 0 = automatic, n = frames per item
     int group_force = 0;
     int n_cu = 0;
@@ -1812,6 +1819,7 @@ int pt_set_tuning(pt_ctx* c, int key, int value) {
     if (value < 0 || value > 64) return fail(c, PT_E_ARG, "threshold must be in 1..64 (0 = automatic)");
     if (key == 0) c->leaf_thresh = value;
     else if (key == 1) c->shade_thresh = value;
+    else if (key == 6) c->trav_floor = value;
     else if (key == 3) {
         if (value != 0 && value != 5 && value != 6) return fail(c, PT_E_ARG, "waves per SIMD must be 5 or 6 (0 = auto)");
         c->minw = value;
@@ -1906,6 +1914,7 @@ static int enqueue_render(pt_ctx* c, int frame_first, int n_frames, int acc_firs
         bool lds_scene = c->lds_bytes <= kLdsSceneMax && c->variant != 3;
         p.leaf_thresh = c->leaf_thresh ? c->leaf_thresh : (lds_scene ? 52 : 16);
         p.shade_thresh = c->shade_thresh ? c->shade_thresh : (lds_scene ? 44 : 32);
+        p.trav_floor = c->trav_floor ? c->trav_floor : (lds_scene ? 8 : 6);
     }
     p.rW = 1.0f / (float)p.W;
     p.rH = 1.0f / (float)p.H;

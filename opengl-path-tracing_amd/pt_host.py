@@ -279,7 +279,8 @@ class PathTracer:
     def set_kernel(self, variant):
         self._check(lib().pt_set_kernel(self.h, int(variant)))
 
-    def set_tuning(self, leaf_thresh=None, shade_thresh=None, adaptive=None, waves_per_simd=None, group=None):
+    def set_tuning(self, leaf_thresh=None, shade_thresh=None, adaptive=None, waves_per_simd=None, group=None,
+                   trav_floor=None):
         if leaf_thresh is not None:
             self._check(lib().pt_set_tuning(self.h, 0, int(leaf_thresh)))
         if shade_thresh is not None:
@@ -290,6 +291,8 @@ class PathTracer:
             self._check(lib().pt_set_tuning(self.h, 3, int(waves_per_simd)))
         if group is not None:
             self._check(lib().pt_set_tuning(self.h, 5, int(group)))
+        if trav_floor is not None:
+            self._check(lib().pt_set_tuning(self.h, 6, int(trav_floor)))
 
     def dispatch(self, frame, accumulate):
         """One glDispatchCompute with uniforms frame/accumulate (ogl_path_trace.h:176-183)."""

@@ -225,17 +225,19 @@ def test_adaptive_tile_order_is_invisible(cornell_scene):
 @pytest.mark.parametrize("rpp", [1, 3])
 def test_occupancy_builds_bitwise(cornell_scene, waves, variant, rpp):
     """Every compiled occupancy (tuning key 3) of the state-machine kernel, LDS and global
-    scene, raysPerPixel 1 and 3, with a few scheduling thresholds."""
+    scene, raysPerPixel 1 and 3, with a few scheduling thresholds and walk floors (64: every
+    walk phase ends after one step batch)."""
     want = O.render(cornell_scene, 48, 40, max_bounce=8, n_frames=5, rpp=rpp)
-    for leaf, shade in ((0, 0), (1, 64), (64, 1)):
+    for leaf, shade, floor in ((0, 0, 0), (1, 64, 1), (64, 1, 1), (64, 64, 64), (40, 40, 24)):
         pt = H.PathTracer(48, 40, max_bounce=8, rays_per_pixel=rpp)
         pt.set_kernel(variant)
-        pt.set_tuning(leaf, shade, waves_per_simd=waves)
+        pt.set_tuning(leaf, shade, waves_per_simd=waves, trav_floor=floor)
         pt.upload(cornell_scene)
         pt.render(1, 5, 0)
         got = pt.read_rgba32f()
         pt.close()
-        assert_bitwise(got, want, "waves %d variant %d rpp %d tune %d:%d" % (waves, variant, rpp, leaf, shade))
+        assert_bitwise(got, want, "waves %d variant %d rpp %d tune %d:%d:%d" % (waves, variant, rpp, leaf, shade,
+                                                                                  floor))
 
 
 def test_aces_epilogue(cornell_scene):
