@@ -181,9 +181,6 @@ PT_HD float logf_bf(float x) {                     // x in {0} U [2^-32, 1]
     const float f = xr - 1.0f;
     const float dk = (float)k;
     const float hi = dk * ln2_hi, lo = dk * ln2_lo;
-    // |f| < 2^-20 branch
-    const float Rs = f * f * (0.5f - 0.33333333333333333f * f);
-    const float small = hi - ((Rs - lo) - f);
     // main branch (2 + f in [1.58, 2.42]: exact reciprocal + Markstein, as logf_pinned)
     const float tf = 2.0f + f;
     const float s = div_mk(f, tf, rcp_fast(tf));
@@ -197,7 +194,17 @@ PT_HD float logf_bf(float x) {                     // x in {0} U [2^-32, 1]
     const float m1 = hi - ((hfsq - (s * (hfsq + R) + lo)) - f);
     const float m2 = hi - ((s * (f - R) - lo) - f);
     float r = ii > 0 ? m1 : m2;
-    r = ((0x007fffff & (0x8000 + ix)) < 0xc000) ? small : r;
+    // |f| < 2^-20 branch (x within ~2^-20 of a power of two: about 1 draw in 2^19), run
+    // only when a lane of the wave needs it
+    const bool is_small = (0x007fffff & (0x8000 + ix)) < 0xc000;
+#if defined(__HIP_DEVICE_COMPILE__)
+    if (__any(is_small))
+#endif
+    {
+        const float Rs = f * f * (0.5f - 0.33333333333333333f * f);
+        const float small = hi - ((Rs - lo) - f);
+        r = is_small ? small : r;
+    }
     return x == 0.0f ? bitsf(0xff800000u) : r;
 }
 PT_HD float cosf_bf(float xx) {                    // finite xx >= 0 (theta in [0, 2*pi])
@@ -239,6 +246,18 @@ PT_HD float sqrt_g(float q) {
     return fsqrt(q);
 }
 PT_HD float length(f3 a) { return sqrt_g(dot(a, a)); }
+// length(a) > 0.01f without the root: RN(sqrt(q)) is non-decreasing in q, and the least
+// binary32 q with RN(sqrt(q)) > 0.01f is 0x38d1b719 (tests/test_exact_div.py checks every
+// binary32 against the IEEE root); NaN fails both forms.
+PT_HD bool length_gt_001(f3 a) { return dot(a, a) >= bitsf(0x38d1b719u); }
+// num / den, correctly rounded: by the exact reciprocal and a Markstein correction when
+// both magnitudes lie in [2^-60, 2^60] (quotient in [2^-120, 2^120], remainder granularity
+// >= 2^-106: no overflow, no underflow), else the IEEE division.
+PT_HD float div_g(float num, float den) {
+    const float an = num < 0.0f ? -num : num, ad = den < 0.0f ? -den : den;
+    if (an >= 0x1p-60f && an <= 0x1p60f && ad >= 0x1p-60f && ad <= 0x1p60f) return div_mk(num, den, rcp_fast(den));
+    return num / den;
+}
 // v * (1/sqrt(dot(v,v))): the two correctly rounded steps, each by its guarded fast form
 // (dot in [2^-100, 2^100] puts the root in [2^-50, 2^50]).
 PT_HD f3 normalize(f3 a) {

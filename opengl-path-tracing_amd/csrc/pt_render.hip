@@ -1128,7 +1128,7 @@ __global__ __launch_bounds__(256, MINW) void k_render_sm(KParams p) {
                 pcost++;
                 bool finished = false;
                 f3 rgb = inc;
-                if (hit && pt::length(col) > 0.01f) {
+                if (hit && pt::length_gt_001(col)) {
                     const f3 hitp = o + d * t;
                     f3 normal;
                     int mat;
@@ -1311,7 +1311,7 @@ __global__ __launch_bounds__(256, MINW) void k_render_sm(KParams p) {
                         float half_b = pt::dot(oc, d);
                         float cq = pt::dot(oc, oc) - s0.w;
                         float disc = half_b * half_b - a * cq;
-                        float ht = disc < 0.0f ? -1.0f : (-half_b - pt::fsqrt(disc)) / a;
+                        float ht = disc < 0.0f ? -1.0f : pt::div_g(-half_b - pt::sqrt_g(disc), a);
                         if (COUNT) c.sph++;
                         if (ht > 0.0001f && ht < t) {
                             t = ht;

@@ -116,3 +116,68 @@ def test_branch_free_box_muller_forms(tmp_path):
     assert out.returncode == 0, out.stdout
     lines = [l for l in out.stdout.splitlines() if "tested=" in l]
     assert len(lines) == 2 and all(" bad=0" in l for l in lines), out.stdout
+
+
+PROG_DIVG = r"""
+#include <math.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+static uint64_t s = 0x853C49E6748FEA9Bull;
+static uint64_t rnd(void) { s ^= s << 13; s ^= s >> 7; s ^= s << 17; return s; }
+static float bf(uint32_t u) { float f; memcpy(&f, &u, 4); return f; }
+static uint32_t fb(float f) { uint32_t u; memcpy(&u, &f, 4); return u; }
+int main(int argc, char** argv) {
+    long long n = atoll(argv[1]), bad = 0;
+    for (long long i = 0; i < n; i++) {
+        uint64_t r = rnd(), r2 = rnd();
+        /* both magnitudes in [2^-60, 2^60]: div_g's fast range (pt_math.h) */
+        float den = bf(((127u - 60u + (uint32_t)(r % 121)) << 23) | (uint32_t)((r >> 8) & 0x7fffff) | (uint32_t)((r >> 40) & 1u) << 31);
+        float num = bf(((127u - 60u + (uint32_t)(r2 % 121)) << 23) | (uint32_t)((r2 >> 8) & 0x7fffff) | (uint32_t)((r2 >> 40) & 1u) << 31);
+        switch ((r2 >> 50) & 7) {
+            case 0: num = den * (float)((r2 >> 20) % 4096 + 1); break;      /* exact multiples */
+            case 1: num = bf(fb(den * 3.0f) + (uint32_t)((r2 >> 20) % 3) - 1u); break;   /* near ties */
+            case 2: den = bf(fb(den) | 0x7fffffu); break;                  /* all-ones mantissa */
+            default: break;
+        }
+        float an = fabsf(num), ad = fabsf(den);
+        if (!(an >= 0x1p-60f && an <= 0x1p60f && ad >= 0x1p-60f && ad <= 0x1p60f)) continue;
+        float rd = 1.0f / den, q0 = num * rd, rem = fmaf(-q0, den, num), q = fmaf(rem, rd, q0);
+        float ex = num / den;
+        if (fb(q) != fb(ex)) { if (bad < 5) printf("num=%a den=%a got %a want %a\n", num, den, q, ex); bad++; }
+    }
+    printf("n=%lld bad=%lld\n", n, bad);
+    return bad != 0;
+}
+"""
+
+
+def test_guarded_division_is_correctly_rounded(tmp_path):
+    """pt_math.h div_g (the sphere root's division in the state-machine kernel): the exact
+    reciprocal + Markstein correction over its guard (both magnitudes in [2^-60, 2^60]),
+    2e7 random pairs incl. exact multiples, near ties and all-ones divisor mantissas."""
+    src = tmp_path / "dg.c"
+    src.write_text(PROG_DIVG)
+    exe = tmp_path / "dg"
+    subprocess.check_call(["gcc", "-O2", "-ffp-contract=off", "-march=x86-64-v3", str(src), "-o", str(exe), "-lm"])
+    out = subprocess.run([str(exe), "20000000"], capture_output=True, text=True)
+    assert out.returncode == 0, out.stdout
+    assert "bad=0" in out.stdout
+
+
+def test_length_threshold_without_root():
+    """pt_math.h length_gt_001: dot(c,c) >= 0x38d1b719 <=> RN(sqrt(dot(c,c))) > 0.01f, for
+    every non-negative binary32 (and NaN), against the IEEE root."""
+    import numpy as np
+    thr = np.uint32(0x38d1b719)
+    step = 1 << 26
+    for base in range(0, 0x7f800001 + step, step):
+        u = np.arange(base, min(base + step, 0x7fc00001), dtype=np.uint32)
+        if u.size == 0:
+            break
+        q = u.view(np.float32)
+        with np.errstate(invalid="ignore"):
+            want = np.sqrt(q) > np.float32(0.01)
+        got = q >= thr.view(np.float32)
+        assert np.array_equal(want, got), hex(int(u[np.argmax(want != got)]))
