@@ -128,7 +128,8 @@ int pt_set_kernel(pt_ctx* ctx, int variant);
  * key 1 = run the shading phase once this many lanes finished their segment (1..64, 0 = auto),
  * key 2 = adaptive tile order (1 default: 8x8 tiles are queued most-expensive-first using
  *         the segment counts of the previous renders; 0 = raster order),
- * key 3 = resident waves per SIMD the kernel is compiled for (5 or 6; 0 = auto),
+ * key 3 = resident waves per SIMD the kernel is compiled for (5..8; 0 = auto: 7 for scenes
+ *         staged in LDS, 6 for global-memory scenes),
  * key 5 = frames per work item (>= 1; 0 = auto, 2..8): a pixel's frames are spread over
  *         several lanes and the running mean is applied by a second kernel in frame order;
  *         a value >= n_frames gives each lane whole pixels (running mean in registers).

@@ -963,7 +963,10 @@ constexpr unsigned kPullBatch = 32;
 #ifndef PT_LEAF_COMPACT
 #define PT_LEAF_COMPACT 1   // leaf phase: edge tests compacted over the wave (leaf_pair_tests)
 #endif
-constexpr int kWalkUnroll = 4;   // node steps per yield check of the walk (measured: 1 -> 2 +3.6%, 4 +5.7%, 6/8 slower)
+#ifndef PT_WALK_UNROLL
+#define PT_WALK_UNROLL 4
+#endif
+constexpr int kWalkUnroll = PT_WALK_UNROLL;   // node steps per yield check of the walk (measured: 1 -> 2 +3.6%, 4 +5.7%, 6/8 slower)
 
 // The TRAV phase: each TRAV lane advances one node per iteration (bvh_intersect + the link
 // choice of calculateRayCollision :389-431) until it stops at a leaf whose box it hit
@@ -1821,7 +1824,7 @@ int pt_set_tuning(pt_ctx* c, int key, int value) {
     else if (key == 1) c->shade_thresh = value;
     else if (key == 6) c->trav_floor = value;
     else if (key == 3) {
-        if (value != 0 && value != 5 && value != 6) return fail(c, PT_E_ARG, "waves per SIMD must be 5 or 6 (0 = auto)");
+        if (value != 0 && (value < 5 || value > 8)) return fail(c, PT_E_ARG, "waves per SIMD must be 5..8 (0 = auto)");
         c->minw = value;
     }
     else if (key == 2) {
@@ -1963,16 +1966,22 @@ static int enqueue_render(pt_ctx* c, int frame_first, int n_frames, int acc_firs
 #define PT_LAUNCH(K, L, MW)                                                                                   \
     if (c->counting) hipLaunchKernelGGL((K<true, L, MW>), grid, dim3(256), L ? lds : 0, c->stream, p);        \
     else hipLaunchKernelGGL((K<false, L, MW>), grid, dim3(256), L ? lds : 0, c->stream, p);
-        // occupancy: 6 waves/SIMD (80 VGPRs) measured best for LDS scenes (+5% on C2 over 5),
-        // a tie for global-memory scenes
-        const int mw = c->minw ? c->minw : 6;
-        const size_t top_lds = (size_t)c->n_top * 2 * sizeof(float4);   // global scene: top nodes
+        // occupancy: 7 waves/SIMD for LDS scenes (72 VGPRs, a few spilled: +0.8% on C2 over
+        // 6, which was +5% over 5; 8 spills 20+ and loses 7%), 6 for global-memory scenes (7
+        // leaves fewer top nodes per block in LDS: -6% on the C3 stand-in)
+        const int mw = c->minw ? c->minw : (use_lds ? 7 : 6);
+        // global scene: the top nodes staged per block, at most what mw blocks per CU fit in
+        // its 160 KiB of LDS (the first K of the breadth-first numbering, any K <= n_top)
+        if (mw > 6) p.n_top = std::min(c->n_top, 160 * 1024 / mw / 32 - 8);
+        const size_t top_lds = (size_t)p.n_top * 2 * sizeof(float4);
 #define PT_LAUNCH_SM(L, M)                                                                                    \
     if (c->counting && p.rgb) hipLaunchKernelGGL((k_render_sm<true, L, 5, M, true>), grid, dim3(256), L ? lds : top_lds, c->stream, p); \
     else if (c->counting) hipLaunchKernelGGL((k_render_sm<true, L, 5, M, false>), grid, dim3(256), L ? lds : top_lds, c->stream, p); \
-    else if (p.rgb && mw == 6) hipLaunchKernelGGL((k_render_sm<false, L, 6, M, true>), grid, dim3(256), L ? lds : top_lds, c->stream, p); \
+    else if (p.rgb && mw == 8 && !M) hipLaunchKernelGGL((k_render_sm<false, L, 8, false, true>), grid, dim3(256), L ? lds : top_lds, c->stream, p); \
+    else if (p.rgb && mw == 7 && !M) hipLaunchKernelGGL((k_render_sm<false, L, 7, false, true>), grid, dim3(256), L ? lds : top_lds, c->stream, p); \
+    else if (p.rgb && mw >= 6) hipLaunchKernelGGL((k_render_sm<false, L, 6, M, true>), grid, dim3(256), L ? lds : top_lds, c->stream, p); \
     else if (p.rgb) hipLaunchKernelGGL((k_render_sm<false, L, 5, M, true>), grid, dim3(256), L ? lds : top_lds, c->stream, p); \
-    else if (mw == 6) hipLaunchKernelGGL((k_render_sm<false, L, 6, M, false>), grid, dim3(256), L ? lds : top_lds, c->stream, p); \
+    else if (mw >= 6) hipLaunchKernelGGL((k_render_sm<false, L, 6, M, false>), grid, dim3(256), L ? lds : top_lds, c->stream, p); \
     else hipLaunchKernelGGL((k_render_sm<false, L, 5, M, false>), grid, dim3(256), L ? lds : top_lds, c->stream, p);
         if (c->variant == 0 || c->variant == 3) {
             bool multi = p.rpp > 1;

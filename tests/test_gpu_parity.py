@@ -220,7 +220,7 @@ def test_adaptive_tile_order_is_invisible(cornell_scene):
     assert_bitwise(imgs[1], imgs[0], "adaptive order")
 
 
-@pytest.mark.parametrize("waves", [5, 6])
+@pytest.mark.parametrize("waves", [5, 6, 7, 8])
 @pytest.mark.parametrize("variant", [0, 3])
 @pytest.mark.parametrize("rpp", [1, 3])
 def test_occupancy_builds_bitwise(cornell_scene, waves, variant, rpp):
