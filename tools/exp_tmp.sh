@@ -1,2 +1,4 @@
 cd "$GRAFT_REPO_ROOT"; mkdir -p gpurun_out
-timeout -k 10 900 python tools/probe.py --spp 128 --variants 0 --chunks 128 --rounds 2 --tunings 52:44:1:7:0:8,56:44:1:7:0:8,60:44:1:7:0:8,56:48:1:7:0:8,56:40:1:7:0:8,52:44:1:7:0:12,56:44:1:7:0:12,60:48:1:7:0:12,48:40:1:7:0:8 > gpurun_out/sweep.log 2>&1; echo "rc=$?"; grep "^round 1" gpurun_out/sweep.log | cut -c1-80
+T=16:24:1:0:0:6,16:16:1:0:0:6,12:24:1:0:0:6,16:20:1:0:0:6,12:16:1:0:0:4,8:16:1:0:0:4,12:20:1:0:0:6,16:12:1:0:0:6
+timeout -k 10 900 python tools/probe.py --scene bunny --spp 64 --variants 0 --chunks 64 --rounds 2 --tunings $T > gpurun_out/sweep3.log 2>&1; echo "rc=$?"; grep "^round 1" gpurun_out/sweep3.log | cut -c1-80
+timeout -k 10 900 python tools/probe.py --scene sponza --spp 32 --variants 0 --chunks 32 --rounds 2 --tunings $T > gpurun_out/sweep4.log 2>&1; echo "rc=$?"; grep "^round 1" gpurun_out/sweep4.log | cut -c1-80
