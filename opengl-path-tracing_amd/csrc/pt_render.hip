@@ -60,7 +60,7 @@ struct KParams {
     int trav_floor;                // ... and the walk floor: fewer walking lanes end a walk phase
     const int* frame_dev;          // progressive graph: device frame counter (null = use frame_first)
     int frame_offset;              // this launch's frame offset from *frame_dev
-    const unsigned* tile_perm;     // queue order of 8x8 tiles (null = raster order)
+    const unsigned* tile_perm;     // queue order of 8x8 tiles, entries (ty << 16) | tx (null = raster order)
     unsigned* tile_cost;           // per-tile segment counts of this launch (null = off)
     // frame-split work items (state-machine kernel): a queue item is (pixel, `group`
     // consecutive frames); with rgb != null the lane stores each frame's pixel colour (12 B)
@@ -70,6 +70,8 @@ struct KParams {
     int group;
     float* rgb;                    // 3 floats per (frame, pixel)
     float rW, rH;                  // RN(1/W), RN(1/H) (host IEEE division) for the camera ray
+    float fW, fH;                  // W, H as binary32 (kernel arguments: uniform, no VGPR)
+    unsigned grp_magic;            // ceil(2^32 / n_groups) when item * n_groups < 2^32 for every item, else 0
     // root box (min.x, max.x, min.y, max.y, min.z, max.z) and its first child (-1: the root is
     // a leaf): a ray starting inside the root box hits it, so the walk may start at the child
     float root_box[6];
@@ -635,6 +637,18 @@ __device__ __forceinline__ bool tri_edges_at(const SceneView& S, int slot, f3 p)
     const float e2 = pt::dot(n, pt::cross(v0 - v2, p - v2));
     return (e0 > 0.0f) && (e1 > 0.0f) && (e2 > 0.0f);
 }
+// The lane's index in its wave, recomputed where it is used (two VALU): a value held across
+// the state-machine loop is spilled to scratch at 7 waves per SIMD, and its reload sat in
+// the leaf and queue paths.  Volatile, so the compiler neither hoists nor merges it.
+__device__ __forceinline__ int lane_id() {
+    int l;
+    asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(l));
+    return l;
+}
+// Number of set bits of m below this lane.
+__device__ __forceinline__ int rank_in(unsigned long long m) {
+    return (int)__builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)m, 0u));
+}
 __device__ __forceinline__ float fperm_f(int dst_bytes, float v) {
     return __int_as_float(__builtin_amdgcn_ds_permute(dst_bytes, __float_as_int(v)));
 }
@@ -655,7 +669,7 @@ __device__ __forceinline__ float fperm_f(int dst_bytes, float v) {
 // Returns (through h1 / h2) the hit_triangle results up to that equivalence.
 template <bool LDS>
 __device__ __forceinline__ void leaf_pair_tests(const SceneView& S, bool at, int s0, float4 q3a, float4 q3b,
-                                                f3 o, f3 d, float t, int lane, float& h1, float& h2) {
+                                                f3 o, f3 d, float t, float& h1, float& h2) {
     float ta = 0.0f, tb = 0.0f;
     if (at) {
         ta = tri_plane<LDS>(S, s0, q3a, o, d);
@@ -667,8 +681,8 @@ __device__ __forceinline__ void leaf_pair_tests(const SceneView& S, bool at, int
     const int ca = __popcll(ma), n = ca + __popcll(mb);
     bool oka = false, okb = false;
     if (n <= 63) {
-        const unsigned long long below = (1ull << lane) - 1ull;
-        const int ja = __popcll(ma & below), jb = ca + __popcll(mb & below);
+        const int lane = lane_id();
+        const int ja = rank_in(ma), jb = ca + rank_in(mb);
         // forward permutes hand worker j its pair's hit point o + d*t and slot; lanes
         // without a pair send to lane 63, never a worker (n <= 63)
         const int da = (na ? ja : 63) << 2, db = (nb ? jb : 63) << 2;
@@ -1071,7 +1085,9 @@ __global__ __launch_bounds__(256, MINW) void k_render_sm(KParams p) {
         S.np = K;
         S.tp = 0;
     }
+#ifdef PT_PHASE_CLOCK
     const int lane = threadIdx.x & 63;
+#endif
     const f3 cpos = mk(p.cam[0], p.cam[1], p.cam[2]), cfwd = mk(p.cam[3], p.cam[4], p.cam[5]);
     const f3 cright = mk(p.cam[6], p.cam[7], p.cam[8]), cup = mk(p.cam[9], p.cam[10], p.cam[11]);
     const int tiles_x = (p.W + 7) >> 3;
@@ -1229,7 +1245,7 @@ __global__ __launch_bounds__(256, MINW) void k_render_sm(KParams p) {
             unsigned long long m = __ballot(want);
             if (m) {
                 const unsigned need = (unsigned)__popcll(m);
-                const unsigned rank = (unsigned)__popcll(m & ((1ull << lane) - 1ull));
+                const unsigned rank = (unsigned)rank_in(m);
                 const int leader = __ffsll((long long)m) - 1;
                 unsigned id;
                 if (SPLIT && qend - qnext >= need) {
@@ -1239,8 +1255,8 @@ __global__ __launch_bounds__(256, MINW) void k_render_sm(KParams p) {
                     const unsigned avail = SPLIT ? qend - qnext : 0u;
                     const unsigned take = SPLIT ? max(need - avail, kPullBatch) : need;
                     unsigned base = 0;
-                    if (lane == leader) base = atomicAdd(p.work_counter, take);
-                    base = __shfl(base, leader, 64);
+                    if (want && rank == 0u) base = atomicAdd(p.work_counter, take);   // the leader
+                    base = (unsigned)__builtin_amdgcn_readlane((int)base, leader);
                     id = rank < avail ? qnext + rank : base + (rank - avail);
                     if (SPLIT) {
                         qnext = base + (need - avail);
@@ -1252,11 +1268,23 @@ __global__ __launch_bounds__(256, MINW) void k_render_sm(KParams p) {
                         st = ST_DONE;
                     } else {
                         const unsigned item = id >> 6, w = id & 63u;
-                        unsigned tile = SPLIT ? item / n_groups : item;
+                        // item -> (tile, frame group): by the host's exact magic reciprocal
+                        // (kernel argument) when it is valid for every item
+                        unsigned tile = item;
+                        if (SPLIT) tile = p.grp_magic ? __umulhi(item, p.grp_magic) : item / n_groups;
                         const int g = SPLIT ? (int)(item - tile * n_groups) : 0;
-                        if (p.tile_perm) tile = p.tile_perm[tile];
-                        int cx = (int)(tile % (unsigned)tiles_x) * 8 + (int)(w & 7u);
-                        int crow = (int)(tile / (unsigned)tiles_x) * 8 + (int)(w >> 3);
+                        int tx, ty;
+                        if (p.tile_perm) {          // packed (ty << 16) | tx: no division
+                            const unsigned pk = p.tile_perm[tile];
+                            tx = (int)(pk & 0xffffu);
+                            ty = (int)(pk >> 16);
+                        } else {
+                            tx = (int)(tile % (unsigned)tiles_x);
+                            ty = (int)(tile / (unsigned)tiles_x);
+                        }
+                        tile = (unsigned)(ty * tiles_x + tx);
+                        int cx = tx * 8 + (int)(w & 7u);
+                        int crow = ty * 8 + (int)(w >> 3);
                         int cy = p.row0 + crow * p.row_stride;
                         if (cx < p.W && crow < p.rows_local && cx < p.x_limit && cy < p.y_limit) {
                             lx = cx;
@@ -1287,8 +1315,8 @@ __global__ __launch_bounds__(256, MINW) void k_render_sm(KParams p) {
                     // (x + jitter) / W by the exact reciprocal RN(1/W) and a Markstein
                     // correction: the numerator is 0 or in [2^-32, 2^17), W <= 2^16, so the
                     // remainder is exact and the quotient correctly rounded (test_exact_div)
-                    float u = pt::div_mk((float)lx + ax, (float)p.W, p.rW) - 0.5f;
-                    float v = pt::div_mk((float)y + ay, (float)p.H, p.rH) - 0.5f;
+                    float u = pt::div_mk((float)lx + ax, p.fW, p.rW) - 0.5f;
+                    float v = pt::div_mk((float)y + ay, p.fH, p.rH) - 0.5f;
                     d = pt::normalize((cfwd + cright * u) + cup * v);
                     o = cpos;
                     inc = mk(0, 0, 0);
@@ -1355,7 +1383,7 @@ __global__ __launch_bounds__(256, MINW) void k_render_sm(KParams p) {
                 }
             } else {
 #if PT_LEAF_COMPACT
-                leaf_pair_tests<LDS>(S, at, s0, q3, at ? tri_quad<LDS>(S, s0 + 1, 3) : q3, o, d, t, lane, h1, h2);
+                leaf_pair_tests<LDS>(S, at, s0, q3, at ? tri_quad<LDS>(S, s0 + 1, 3) : q3, o, d, t, h1, h2);
 #else
                 if (at) {
                     f3 n0, n1;
@@ -1465,7 +1493,7 @@ struct pt_ctx {
     // previous renders order the next render's 8x8 tiles so cheap tiles form the tail
     unsigned* d_tile_cost = nullptr;
     unsigned* d_tile_perm = nullptr;
-    int n_tiles = 0;
+    int n_tiles = 0, tiles_x = 1;
     bool adaptive = true, cost_pending = false;
     hipGraph_t graph = nullptr;
     hipGraphExec_t graph_exec = nullptr;
@@ -1493,6 +1521,13 @@ struct pt_ctx {
     bool count_pending = false;
     std::string err;
 };
+
+// Queue-order entry of linear tile t (row-major 8x8 tiles): (ty << 16) | tx, so the kernel
+// decodes a tile without an integer division.
+static unsigned pack_tile(const pt_ctx* c, unsigned t) {
+    return ((t / (unsigned)c->tiles_x) << 16) | (t % (unsigned)c->tiles_x);
+}
+
 
 static void drop_graph(pt_ctx* c);   // a captured graph bakes in scene/camera/config
 
@@ -1549,9 +1584,10 @@ int pt_create(const pt_config* cfg, pt_ctx** out) {
     c->persist_blocks = (unsigned)std::max(1, n_cu) * 8u;   // 8 x 256 threads = 32 waves per CU
     c->n_cu = std::max(1, n_cu);
     c->n_tiles = ((cfg->width + 7) / 8) * ((c->rows_local + 7) / 8);
+    c->tiles_x = (cfg->width + 7) / 8;
     {
         std::vector<unsigned> ident(std::max(c->n_tiles, 1));
-        for (size_t i = 0; i < ident.size(); i++) ident[i] = (unsigned)i;
+        for (size_t i = 0; i < ident.size(); i++) ident[i] = pack_tile(c, (unsigned)i);
         HIPCHK(c, hipMalloc(&c->d_tile_perm, ident.size() * sizeof(unsigned)));
         HIPCHK(c, hipMalloc(&c->d_tile_cost, ident.size() * sizeof(unsigned)));
         HIPCHK(c, hipMemcpy(c->d_tile_perm, ident.data(), ident.size() * sizeof(unsigned), hipMemcpyHostToDevice));
@@ -1832,7 +1868,7 @@ int pt_set_tuning(pt_ctx* c, int key, int value) {
         c->adaptive = value != 0;
         if (!c->adaptive && c->n_tiles > 0) {       // back to raster order
             std::vector<unsigned> ident(c->n_tiles);
-            for (int i = 0; i < c->n_tiles; i++) ident[i] = (unsigned)i;
+            for (int i = 0; i < c->n_tiles; i++) ident[i] = pack_tile(c, (unsigned)i);
             HIPCHK(c, hipMemcpy(c->d_tile_perm, ident.data(), ident.size() * sizeof(unsigned), hipMemcpyHostToDevice));
             c->cost_pending = false;
         }
@@ -1921,8 +1957,16 @@ static int enqueue_render(pt_ctx* c, int frame_first, int n_frames, int acc_firs
         p.trav_floor = c->trav_floor ? c->trav_floor : (lds_scene ? 8 : 6);
     }
     p.rW = 1.0f / (float)p.W;
+    p.fW = (float)p.W;
+    p.fH = (float)p.H;
     p.rH = 1.0f / (float)p.H;
     p.group = plan_group(c, n_frames);
+    {   // exact item / n_groups by ceil(2^32 / n_groups) when item * n_groups < 2^32 for every
+        // item (then floor(item * m / 2^32) = floor(item / n_groups)), else the division
+        const unsigned long long ng = (unsigned long long)((n_frames + p.group - 1) / p.group);
+        const unsigned long long items = (unsigned long long)c->n_tiles * ng;
+        p.grp_magic = (ng > 1 && items * ng < (1ull << 32)) ? (unsigned)(((1ull << 32) + ng - 1) / ng) : 0u;
+    }
     if (p.group < n_frames) {
         int rc = ensure_rgb(c, n_frames);
         if (rc) return rc;
@@ -2113,7 +2157,7 @@ int pt_sync(pt_ctx* c) {
         auto bucket = [&](unsigned v) { return nb - 1 - (int)((unsigned long long)v * (nb - 1) / mx); };
         for (unsigned v : cost) cnt[bucket(v) + 1]++;
         for (int b = 0; b < nb; b++) cnt[b + 1] += cnt[b];
-        for (int t = 0; t < c->n_tiles; t++) perm[cnt[bucket(cost[t])]++] = (unsigned)t;
+        for (int t = 0; t < c->n_tiles; t++) perm[cnt[bucket(cost[t])]++] = pack_tile(c, (unsigned)t);
         HIPCHK(c, hipMemcpy(c->d_tile_perm, perm.data(), c->n_tiles * sizeof(unsigned), hipMemcpyHostToDevice));
         HIPCHK(c, hipMemset(c->d_tile_cost, 0, c->n_tiles * sizeof(unsigned)));
         c->cost_pending = false;
