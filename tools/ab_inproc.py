@@ -1,0 +1,80 @@
+"""Same-process A/B timing of library builds: every build is loaded into ONE process (its own
+ctypes handle through its own copy of pt_host), and their renders are interleaved round by
+round, so clock and thermal drift between processes does not enter the comparison.
+
+python tools/ab_inproc.py --libs base,cur --rounds 4 --spp 128 --chunk 128 [--scene bunny]
+('cur' = build/libptrace.so, other names = build/libptrace_<name>.so from tools/ab_build.sh)
+"""
+import argparse
+import importlib.util
+import os
+import statistics
+import sys
+import time
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+PKG = os.path.join(REPO, "opengl-path-tracing_amd")
+sys.path.insert(0, PKG)
+import pt_scenes  # noqa: E402
+
+
+def load_host(name):
+    path = os.path.join(PKG, "build", "libptrace.so" if name == "cur" else "libptrace_%s.so" % name)
+    os.environ["PT_LIB"] = path
+    spec = importlib.util.spec_from_file_location("pt_host_" + name, os.path.join(PKG, "pt_host.py"))
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    assert mod.LIB_PATH == path
+    return mod
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--libs", default="base,cur")
+    ap.add_argument("--rounds", type=int, default=4)
+    ap.add_argument("--spp", type=int, default=128)
+    ap.add_argument("--chunk", type=int, default=128)
+    ap.add_argument("--scene", default="cornell")
+    ap.add_argument("--width", type=int, default=1920)
+    ap.add_argument("--height", type=int, default=1080)
+    a = ap.parse_args()
+    libs = a.libs.split(",")
+    hosts = {l: load_host(l) for l in libs}
+    obj, mtl = pt_scenes.write_scene(a.scene, os.path.join(REPO, "scenes"))
+    pts, seg = {}, {}
+    for l in libs:
+        H = hosts[l]
+        pt = H.PathTracer(a.width, a.height, max_bounce=8)
+        pt.upload(H.setupBuffers(obj, mtl))
+        pt.set_counting(True)
+        total = 0
+        for f0 in range(1, a.spp + 1, a.chunk):
+            pt.render(f0, min(a.chunk, a.spp - f0 + 1), 0 if f0 == 1 else 1)
+            total += pt.stats()[1]["segments"]
+        pt.set_counting(False)
+        pts[l], seg[l] = pt, total
+    if len(set(seg.values())) != 1:
+        print("segment counts differ between builds: %s" % seg)
+        sys.exit(1)
+    res = {l: [] for l in libs}
+    for rnd in range(a.rounds + 1):             # round 0 warms every build up
+        for l in libs:
+            pt = pts[l]
+            t0 = time.perf_counter()
+            for f0 in range(1, a.spp + 1, a.chunk):
+                pt.render_async(f0, min(a.chunk, a.spp - f0 + 1), 0 if f0 == 1 else 1)
+            pt.sync()
+            dt = time.perf_counter() - t0
+            if rnd:
+                res[l].append(seg[l] / dt / 1e6)
+                print("round %d %-8s %9.1f Mrays/s" % (rnd, l, res[l][-1]), flush=True)
+    base = statistics.median(res[libs[0]])
+    for l in libs:
+        m = statistics.median(res[l])
+        print("%-8s median %9.1f  best %9.1f  (%+.2f%% vs %s)" % (l, m, max(res[l]), 100.0 * (m / base - 1.0), libs[0]))
+    for pt in pts.values():
+        pt.close()
+
+
+if __name__ == "__main__":
+    main()
