@@ -55,6 +55,7 @@ struct KParams {
     unsigned int* work_counter;    // persistent kernel pixel queue
     int n_slots, n_mats;           // triangle slots / materials (LDS staging sizes)
     int n_top;                     // global-memory scene: nodes [0, n_top) staged in LDS
+    int walk_np;                   // LDS walk image: nodes per image plane (n_nodes, or kPadNodes)
     int scene_fast;                // every box coordinate inside the exact-reciprocal guard
     int leaf_thresh, shade_thresh; // wave scheduling thresholds of the state-machine kernel
     int trav_floor;                // ... and the walk floor: fewer walking lanes end a walk phase
@@ -427,13 +428,19 @@ struct SceneView {
 // The global-memory walk keeps the reference links (node indices, a = ~code at a leaf):
 // there the loads, not the selects, set the pace, and the reference form measured faster.
 extern __shared__ float4 g_lds[];   // the state-machine kernel's scene copy (nodes first)
+// Scenes of at most kPadNodes nodes get walk images padded to kPadNodes nodes per plane, so
+// the hi half of a node sits at the compile-time offset 16 * kPadNodes from its lo half (an
+// immediate ds_read_b128 offset instead of an address add per walk step).  67: consecutive
+// images start 134 16-B granules apart, 6 mod 16, spreading them over the LDS bank groups.
+constexpr int kPadNodes = 67;
 typedef float v4f __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) const v4f lds_v4f;
-template <bool LDS>
+template <bool LDS, bool PADN = false>
 __device__ __forceinline__ void node_at(const SceneView& S, int i, float4& lo, float4& hi) {
     if (LDS) {      // i = byte offset from the LDS base, which is 0 (checked at kernel entry)
         const v4f x = *(lds_v4f*)(size_t)(unsigned)i;
-        const v4f y = *(lds_v4f*)(size_t)(unsigned)(i + (S.np << 4));
+        const v4f y = PADN ? *(lds_v4f*)(size_t)((unsigned)i + 16u * kPadNodes)
+                           : *(lds_v4f*)(size_t)(unsigned)(i + (S.np << 4));
         lo = make_float4(x.x, x.y, x.z, x.w);
         hi = make_float4(y.x, y.y, y.z, y.w);
     } else if (i < S.np) {   // global-memory scene: a top node, staged in LDS
@@ -992,7 +999,7 @@ constexpr int kWalkUnroll = PT_WALK_UNROLL;   // node steps per yield check of t
 // accepted scene -- pt_upload_scene rejects link graphs with a cycle, and a walk in an
 // acyclic graph visits each node at most once.  The transition is select-only; `leaf`
 // keeps the raw link (~code), decoded in LEAF.
-template <bool ALL_FAST, bool COUNT, bool LDS>
+template <bool ALL_FAST, bool COUNT, bool LDS, bool PADN>
 __device__ __forceinline__ void trav_walk(const SceneView& S, f3 o, f3 d, f3 rd, bool fast, float t,
                                           unsigned long long live, int leaf_thresh, int shade_thresh,
                                           int trav_floor, int& st, int& bi, int& leaf, Cnt& c) {
@@ -1007,7 +1014,7 @@ __device__ __forceinline__ void trav_walk(const SceneView& S, f3 o, f3 d, f3 rd,
     auto step = [&]() {
         if (w >= 0) {
             float4 lo, hi;
-            node_at<LDS>(S, w, lo, hi);
+            node_at<LDS, PADN>(S, w, lo, hi);
             int a = __float_as_int(hi.z), b = __float_as_int(hi.w);
             bool hb = (ALL_FAST || fast) ? (LDS ? slab_oct(lo, hi, o, d, rd, t) : slab_fast(lo, hi, o, d, rd, t))
                                          : slab(lo, hi, o, d, t);
@@ -1051,7 +1058,7 @@ __device__ __forceinline__ void trav_walk(const SceneView& S, f3 o, f3 d, f3 rd,
 __device__ unsigned long long g_phase_clk[8];
 #endif
 
-template <bool COUNT, bool LDS, int MINW, bool MULTI, bool SPLIT>
+template <bool COUNT, bool LDS, int MINW, bool MULTI, bool SPLIT, bool PADN = false>
 __global__ __launch_bounds__(256, MINW) void k_render_sm(KParams p) {
     resolve_frames(p);
     extern __shared__ float4 lds[];
@@ -1059,7 +1066,7 @@ __global__ __launch_bounds__(256, MINW) void k_render_sm(KParams p) {
     if (LDS) {      // planes (see node_at / tri_quad)
         // node_at addresses LDS by raw offset: the dynamic LDS block must start at offset 0
         if ((unsigned)(size_t)(__attribute__((address_space(3))) const char*)g_lds != 0u) __builtin_trap();
-        const int N = p.sc.n_nodes, T = p.n_slots, nn = 16 * N, nt = 4 * T;   // 8 octant images
+        const int N = PADN ? kPadNodes : p.walk_np, T = p.n_slots, nn = 16 * N, nt = 4 * T;   // 8 octant images
         const int nm = 3 * p.n_mats, ns = 2 * p.sc.n_spheres;
         for (int i = threadIdx.x; i < nn; i += blockDim.x) lds[i] = p.sc.walk_lds[i];   // ready-made image
         for (int i = threadIdx.x; i < nt; i += blockDim.x) lds[nn + (i & 3) * T + (i >> 2)] = p.sc.tris[i];
@@ -1409,9 +1416,9 @@ __global__ __launch_bounds__(256, MINW) void k_render_sm(KParams p) {
             // the per-node IEEE-division branch.
             const unsigned long long live = __ballot(st != ST_DONE);
             if (__all(fast || st != ST_TRAV))
-                trav_walk<true, COUNT, LDS>(S, o, d, rd, fast, t, live, p.leaf_thresh, p.shade_thresh, p.trav_floor, st, bi, leaf, c);
+                trav_walk<true, COUNT, LDS, PADN>(S, o, d, rd, fast, t, live, p.leaf_thresh, p.shade_thresh, p.trav_floor, st, bi, leaf, c);
             else
-                trav_walk<false, COUNT, LDS>(S, o, d, rd, fast, t, live, p.leaf_thresh, p.shade_thresh, p.trav_floor, st, bi, leaf, c);
+                trav_walk<false, COUNT, LDS, PADN>(S, o, d, rd, fast, t, live, p.leaf_thresh, p.shade_thresh, p.trav_floor, st, bi, leaf, c);
         }
 #ifdef PT_PHASE_CLOCK
         clk[clk_ph] += clock64() - clk_t0;
@@ -1498,7 +1505,7 @@ struct pt_ctx {
     hipGraph_t graph = nullptr;
     hipGraphExec_t graph_exec = nullptr;
     int graph_frames = 0;
-    int n_nodes = 0, n_spheres = 0, n_mats = 0, n_slots = 0, scene_fast = 0, n_top = 0;
+    int n_nodes = 0, n_spheres = 0, n_mats = 0, n_slots = 0, scene_fast = 0, n_top = 0, walk_np = 1;
     float root_box[6] = {0, 0, 0, 0, 0, 0};
     int root_child = -1;
     size_t lds_bytes = 0;
@@ -1753,8 +1760,8 @@ int pt_upload_scene(pt_ctx* c, const float* tris, int n_tris, const float* bvh, 
     // octant k the node planes (bounds of the axes whose bit is set in k swapped) with links
     // as byte offsets (16 * (2N * k + index)) and a leaf's hit link -2 - code; the leaf's
     // next-right (image-0 offset) goes to its first triangle's quad 3 .z
-    const size_t N = (size_t)std::max(n_nodes, 1);
-    std::vector<float4> dwl(16 * N);
+    const size_t N = (size_t)(n_nodes <= kPadNodes ? kPadNodes : n_nodes);   // nodes per image plane
+    std::vector<float4> dwl(16 * N, make_float4(0, 0, 0, 0));
     for (int k = 0; k < 8; k++) {
         const int base = 16 * 2 * (int)N * k;
         for (int i = 0; i < n_nodes; i++) {
@@ -1804,7 +1811,8 @@ int pt_upload_scene(pt_ctx* c, const float* tris, int n_tris, const float* bvh, 
         }
         if (!(nd[0] <= nd[4] && nd[1] <= nd[5] && nd[2] <= nd[6])) c->scene_fast = 0;
     }
-    c->lds_bytes = (size_t)(16 * n_nodes + 4 * c->n_slots + 3 * n_mats + 2 * n_spheres) * sizeof(float4);
+    c->walk_np = (int)N;
+    c->lds_bytes = (size_t)(16 * N + 4 * c->n_slots + 3 * n_mats + 2 * n_spheres) * sizeof(float4);
     c->root_child = -1;
     if (n_nodes > 0) {
         const float4 r0 = dn[0], r1 = dn[1];
@@ -1946,6 +1954,7 @@ static int enqueue_render(pt_ctx* c, int frame_first, int n_frames, int acc_firs
     p.work_counter = c->d_work;
     p.n_slots = c->n_slots;
     p.n_top = c->n_top;
+    p.walk_np = c->walk_np;
     p.n_mats = c->n_mats;
     p.scene_fast = c->scene_fast;
     std::memcpy(p.root_box, c->root_box, sizeof(p.root_box));
@@ -2023,6 +2032,7 @@ static int enqueue_render(pt_ctx* c, int frame_first, int n_frames, int acc_firs
     if (c->counting && p.rgb) hipLaunchKernelGGL((k_render_sm<true, L, 5, M, true>), grid, dim3(256), L ? lds : top_lds, c->stream, p); \
     else if (c->counting) hipLaunchKernelGGL((k_render_sm<true, L, 5, M, false>), grid, dim3(256), L ? lds : top_lds, c->stream, p); \
     else if (p.rgb && mw == 8 && !M) hipLaunchKernelGGL((k_render_sm<false, L, 8, false, true>), grid, dim3(256), L ? lds : top_lds, c->stream, p); \
+    else if (p.rgb && mw == 7 && !M && L && c->walk_np == kPadNodes) hipLaunchKernelGGL((k_render_sm<false, true, 7, false, true, true>), grid, dim3(256), lds, c->stream, p); \
     else if (p.rgb && mw == 7 && !M) hipLaunchKernelGGL((k_render_sm<false, L, 7, false, true>), grid, dim3(256), L ? lds : top_lds, c->stream, p); \
     else if (p.rgb && mw >= 6) hipLaunchKernelGGL((k_render_sm<false, L, 6, M, true>), grid, dim3(256), L ? lds : top_lds, c->stream, p); \
     else if (p.rgb) hipLaunchKernelGGL((k_render_sm<false, L, 5, M, true>), grid, dim3(256), L ? lds : top_lds, c->stream, p); \

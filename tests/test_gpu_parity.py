@@ -185,6 +185,26 @@ def test_large_scene_bitwise(big_scene, variant):
     assert_bitwise(got, want, "large scene")
 
 
+@pytest.mark.parametrize("target", [20, 80])
+def test_mid_size_lds_scene_bitwise(target, tmp_path):
+    """Scenes staged in LDS with more nodes than the padded walk image (kPadNodes = 67):
+    the image planes are then n_nodes apart and the walk computes the hi-half address at run
+    time (Cornell, 35 nodes, takes the padded compile-time path)."""
+    import pt_scenes
+    sc = H.setupBuffers(*pt_scenes.write_scene("bunny", str(tmp_path), target_tris=target))
+    n_nodes = len(np.asarray(sc["nodes"]).reshape(-1, 12))
+    assert 67 < n_nodes <= 160, n_nodes
+    want = O.render(sc, 64, 48, max_bounce=8, n_frames=3)
+    for waves in (6, 7):
+        pt = H.PathTracer(64, 48, max_bounce=8)
+        pt.set_tuning(waves_per_simd=waves)
+        pt.upload(sc)
+        pt.render(1, 3, 0)
+        got = pt.read_rgba32f()
+        pt.close()
+        assert_bitwise(got, want, "mid-size LDS scene, %d tris, %d waves" % (target, waves))
+
+
 def test_progressive_graph_replay(cornell_scene, V):
     """hipGraph-captured sample loop with a device frame counter == pt_render(1, N, 0)."""
     pt = H.PathTracer(40, 24, max_bounce=8)
