@@ -467,7 +467,11 @@ __device__ __forceinline__ float qdiv(float a, float b, float rb) {
 
 __device__ __forceinline__ bool in_guard(float v, float lo, float hi) {
     float a = __builtin_fabsf(v);
-    return v == 0.0f || (a >= lo && a <= hi);
+    return (v == 0.0f) | ((a >= lo) & (a <= hi));
+}
+__device__ __forceinline__ bool in_range_abs(float v, float lo, float hi) {
+    float a = __builtin_fabsf(v);
+    return (a >= lo) & (a <= hi);
 }
 
 // Scalar on purpose: packed f32 (v_pk_fma_f32) takes two passes on gfx950's SIMD-32, so
@@ -1332,9 +1336,12 @@ __global__ __launch_bounds__(256, MINW) void k_render_sm(KParams p) {
                     need_ray = false;
                 }
                 // segment set-up: exact-reciprocal guard, spheres (:372-385), walk start
-                fast = p.scene_fast && in_guard(o.x, 0x1p-40f, 0x1p60f) && in_guard(o.y, 0x1p-40f, 0x1p60f) &&
-                       in_guard(o.z, 0x1p-40f, 0x1p60f) && in_guard(d.x, 0x1p-20f, 2.0f) && d.x != 0.0f &&
-                       in_guard(d.y, 0x1p-20f, 2.0f) && d.y != 0.0f && in_guard(d.z, 0x1p-20f, 2.0f) && d.z != 0.0f;
+                // the ray half of the guard, evaluated without short-circuit branches (each
+                // && of the old form was an exec-mask branch): every origin component 0 or
+                // in [2^-40, 2^60], every direction component in [2^-20, 2] (NaN fails)
+                fast = (p.scene_fast != 0) & in_guard(o.x, 0x1p-40f, 0x1p60f) & in_guard(o.y, 0x1p-40f, 0x1p60f) &
+                       in_guard(o.z, 0x1p-40f, 0x1p60f) & in_range_abs(d.x, 0x1p-20f, 2.0f) &
+                       in_range_abs(d.y, 0x1p-20f, 2.0f) & in_range_abs(d.z, 0x1p-20f, 2.0f);
                 // under the guard |d_i| is in [2^-20, 2]: rcp_fast is the exact RN(1/d_i)
                 if (fast) rd = mk(pt::rcp_fast(d.x), pt::rcp_fast(d.y), pt::rcp_fast(d.z));
                 if (COUNT && !fast) c.slow++;
@@ -1361,9 +1368,9 @@ __global__ __launch_bounds__(256, MINW) void k_render_sm(KParams p) {
                 const bool walk = use_tris && (COUNT || !ray_has_nan(o, d));
                 // inside the root box (all three axes, inclusive) each axis has near <= 0 <=
                 // far, so the exact slab says hit for any t >= 0: skip the root's test
-                const bool inside = root_skip >= 0 && fast && o.x >= p.root_box[0] && o.x <= p.root_box[1] &&
-                                    o.y >= p.root_box[2] && o.y <= p.root_box[3] && o.z >= p.root_box[4] &&
-                                    o.z <= p.root_box[5];
+                const bool inside = (root_skip >= 0) & fast & (o.x >= p.root_box[0]) & (o.x <= p.root_box[1]) &
+                                    (o.y >= p.root_box[2]) & (o.y <= p.root_box[3]) & (o.z >= p.root_box[4]) &
+                                    (o.z <= p.root_box[5]);
                 const int img = (LDS && fast) ? oct_base(d, S.np << 5) : 0;   // octant image
                 bi = walk ? (inside ? root_skip : 0) + img : -1;
                 st = walk ? ST_TRAV : ST_SHADE;

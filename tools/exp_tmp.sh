@@ -1,8 +1,4 @@
 cd "$GRAFT_REPO_ROOT"; mkdir -p gpurun_out
-L=$GRAFT_REPO_ROOT/opengl-path-tracing_amd/build/libptrace_${EXP_LIB}.so
-PT_LIB=$L timeout -k 10 600 python -u -m pytest tests/test_gpu_parity.py -q -m gpu -x --timeout 300 > gpurun_out/exp_tests.log 2>&1; rc=$?
-echo "pytest($EXP_LIB) rc=$rc"; tail -2 gpurun_out/exp_tests.log; [ $rc -eq 0 ] || exit $rc
-timeout -k 10 400 python tools/ab.py --libs cur,${EXP_LIB} --rounds 2 -- --scene bunny --spp 64 --variants 0 --chunks 64 --rounds 2 > gpurun_out/ab_c3.log 2>&1 || exit $?
-echo "C3:"; grep -v amdgpu.ids gpurun_out/ab_c3.log | tail -6
-timeout -k 10 400 python tools/ab.py --libs cur,${EXP_LIB} --rounds 2 -- --scene sponza --spp 32 --variants 0 --chunks 32 --rounds 2 > gpurun_out/ab_c4.log 2>&1 || exit $?
-echo "C4:"; grep -v amdgpu.ids gpurun_out/ab_c4.log | tail -6
+T=16:24:1:6:0:6,16:24:1:7:0:6,16:24:1:8:0:6
+timeout -k 10 900 python tools/probe.py --scene bunny --spp 64 --variants 0 --chunks 64 --rounds 2 --tunings $T > gpurun_out/sweep3.log 2>&1; echo "rc=$?"; grep "^round 1" gpurun_out/sweep3.log | cut -c1-80
+timeout -k 10 900 python tools/probe.py --scene sponza --spp 32 --variants 0 --chunks 32 --rounds 2 --tunings $T > gpurun_out/sweep4.log 2>&1; echo "rc=$?"; grep "^round 1" gpurun_out/sweep4.log | cut -c1-80
