@@ -159,7 +159,7 @@ __device__ __forceinline__ float tri_hit(const float4* T, f3 o, f3 d, float tbes
 // the tail of its launch) -- so the render kernels skip the walk; its result (no hit, t =
 // +inf) is the reference's.  Counting builds still walk, to count the node visits.
 __device__ __forceinline__ bool ray_has_nan(f3 o, f3 d) {
-    return o.x != o.x || o.y != o.y || o.z != o.z || d.x != d.x || d.y != d.y || d.z != d.z;
+    return (o.x != o.x) | (o.y != o.y) | (o.z != o.z) | (d.x != d.x) | (d.y != d.y) | (d.z != d.z);
 }
 
 // RayIntersectsTriangle (computeShader.c:228-272), Moller-Trumbore with EPSILON 1e-7: the
@@ -636,7 +636,7 @@ __device__ __forceinline__ bool tri_edges(const SceneView& S, int slot, f3 o, f3
     const float e0 = pt::dot(n, pt::cross(v1 - v0, p - v0));
     const float e1 = pt::dot(n, pt::cross(v2 - v1, p - v1));
     const float e2 = pt::dot(n, pt::cross(v0 - v2, p - v2));
-    return (e0 > 0.0f) && (e1 > 0.0f) && (e2 > 0.0f);
+    return (e0 > 0.0f) & (e1 > 0.0f) & (e2 > 0.0f);
 }
 template <bool LDS>
 __device__ __forceinline__ bool tri_edges_at(const SceneView& S, int slot, f3 p) {
@@ -646,7 +646,7 @@ __device__ __forceinline__ bool tri_edges_at(const SceneView& S, int slot, f3 p)
     const float e0 = pt::dot(n, pt::cross(v1 - v0, p - v0));
     const float e1 = pt::dot(n, pt::cross(v2 - v1, p - v1));
     const float e2 = pt::dot(n, pt::cross(v0 - v2, p - v2));
-    return (e0 > 0.0f) && (e1 > 0.0f) && (e2 > 0.0f);
+    return (e0 > 0.0f) & (e1 > 0.0f) & (e2 > 0.0f);
 }
 // The lane's index in its wave, recomputed where it is used (two VALU): a value held across
 // the state-machine loop is spilled to scratch at 7 waves per SIMD, and its reload sat in
@@ -686,8 +686,8 @@ __device__ __forceinline__ void leaf_pair_tests(const SceneView& S, bool at, int
         ta = tri_plane<LDS>(S, s0, q3a, o, d);
         tb = tri_plane<LDS>(S, s0 + 1, q3b, o, d);
     }
-    const bool na = at && ta > 0.0001f && ta < t;
-    const bool nb = at && tb >= 0.0001f && tb < t;
+    const bool na = at & (ta > 0.0001f) & (ta < t);
+    const bool nb = at & (tb >= 0.0001f) & (tb < t);
     const unsigned long long ma = __ballot(na), mb = __ballot(nb);
     const int ca = __popcll(ma), n = ca + __popcll(mb);
     bool oka = false, okb = false;
@@ -709,8 +709,8 @@ __device__ __forceinline__ void leaf_pair_tests(const SceneView& S, bool at, int
         bool pass = false;
         if (lane < n) pass = tri_edges_at<LDS>(S, ws, wp);
         const unsigned long long r = __ballot(pass);
-        oka = na && ((r >> ja) & 1ull);
-        okb = nb && ((r >> jb) & 1ull);
+        oka = na & (((r >> ja) & 1ull) != 0ull);
+        okb = nb & (((r >> jb) & 1ull) != 0ull);
     } else {
         if (na) oka = tri_edges<LDS>(S, s0, o, d, ta);
         if (nb) okb = tri_edges<LDS>(S, s0 + 1, o, d, tb);
@@ -1244,7 +1244,7 @@ __global__ __launch_bounds__(256, MINW) void k_render_sm(KParams p) {
                 }
                 fresh = true;
             }
-            if (st == ST_SHADE && need_ray && lx >= 0 && k >= (SPLIT ? kend : p.n_frames)) {
+            if ((st == ST_SHADE) & need_ray & (lx >= 0) & (k >= (SPLIT ? kend : p.n_frames))) {
                 if (!SPLIT) p.accum[aidx] = acc;
                 if (p.tile_cost && tile_id != ~0u) atomicAdd(&p.tile_cost[tile_id], pcost);
                 lx = -1;
@@ -1297,7 +1297,7 @@ __global__ __launch_bounds__(256, MINW) void k_render_sm(KParams p) {
                         int cx = tx * 8 + (int)(w & 7u);
                         int crow = ty * 8 + (int)(w >> 3);
                         int cy = p.row0 + crow * p.row_stride;
-                        if (cx < p.W && crow < p.rows_local && cx < p.x_limit && cy < p.y_limit) {
+                        if ((cx < p.W) & (crow < p.rows_local) & (cx < p.x_limit) & (cy < p.y_limit)) {
                             lx = cx;
                             y = cy;
                             aidx = crow * p.W + cx;
@@ -1358,14 +1358,14 @@ __global__ __launch_bounds__(256, MINW) void k_render_sm(KParams p) {
                         float disc = half_b * half_b - a * cq;
                         float ht = disc < 0.0f ? -1.0f : pt::div_g(-half_b - pt::sqrt_g(disc), a);
                         if (COUNT) c.sph++;
-                        if (ht > 0.0001f && ht < t) {
+                        if ((ht > 0.0001f) & (ht < t)) {
                             t = ht;
                             hprim = -2 - si;
                         }
                     }
                 }
                 fresh = false;
-                const bool walk = use_tris && (COUNT || !ray_has_nan(o, d));
+                const bool walk = use_tris & (COUNT || !ray_has_nan(o, d));
                 // inside the root box (all three axes, inclusive) each axis has near <= 0 <=
                 // far, so the exact slab says hit for any t >= 0: skip the root's test
                 const bool inside = (root_skip >= 0) & fast & (o.x >= p.root_box[0]) & (o.x <= p.root_box[1]) &
@@ -1386,7 +1386,7 @@ __global__ __launch_bounds__(256, MINW) void k_render_sm(KParams p) {
                 s0 = code & ~1;                              // slots 2k, 2k+1
                 q3 = tri_quad<LDS>(S, s0, 3);                // .z / .w: the leaf's next-right
                 cont = LDS ? __float_as_int(q3.z) : bi;      // LDS: offset in image 0
-                if (LDS && fast && cont >= 0) cont += oct_base(d, S.np << 5);
+                if (LDS && (fast & (cont >= 0))) cont += oct_base(d, S.np << 5);
             }
             float h1 = -1.0f, h2 = -1.0f;
             if (p.flags & PT_FLAG_MOLLER_TRUMBORE) {   // wave-uniform
@@ -1407,9 +1407,9 @@ __global__ __launch_bounds__(256, MINW) void k_render_sm(KParams p) {
 #endif
             }
             if (at) {
-                bool c1 = h1 > 0.0001f && h1 < t && (h1 < h2 || h2 < 0.0001f);
-                bool c2 = !c1 && h2 > 0.0001f && h2 < t;
-                if (c1 || c2) {
+                const bool c1 = (h1 > 0.0001f) & (h1 < t) & ((h1 < h2) | (h2 < 0.0001f));
+                const bool c2 = !c1 & (h2 > 0.0001f) & (h2 < t);
+                if (c1 | c2) {
                     t = c1 ? h1 : h2;
                     hprim = s0 + (c1 ? 0 : 1);
                 }
