@@ -135,6 +135,9 @@ int pt_set_kernel(pt_ctx* ctx, int variant);
  *         a value >= n_frames gives each lane whole pixels (running mean in registers).
  * key 6 = walk floor (1..64, 0 = auto): a walk phase ends once fewer lanes than this still
  *         walk, and the leaf (or shading) phase runs even below its threshold.
+ * key 7 = leaf-phase compaction limit (0..63, default 63): the edge tests of a wave's leaf
+ *         phase are packed onto its first lanes when at most this many (lane, triangle) pairs
+ *         need them; 0 = every lane tests its own triangles.
  * None of these change the image (each pixel's frames stay in order in one lane). */
 int pt_set_tuning(pt_ctx* ctx, int key, int value);
 

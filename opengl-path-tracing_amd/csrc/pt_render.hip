@@ -59,6 +59,7 @@ struct KParams {
     int scene_fast;                // every box coordinate inside the exact-reciprocal guard
     int leaf_thresh, shade_thresh; // wave scheduling thresholds of the state-machine kernel
     int trav_floor;                // ... and the walk floor: fewer walking lanes end a walk phase
+    int compact_max;               // leaf phase: compact the edge tests of at most this many pairs (<= 63)
     const int* frame_dev;          // progressive graph: device frame counter (null = use frame_first)
     int frame_offset;              // this launch's frame offset from *frame_dev
     const unsigned* tile_perm;     // queue order of 8x8 tiles, entries (ty << 16) | tx (null = raster order)
@@ -680,7 +681,7 @@ __device__ __forceinline__ float fperm_f(int dst_bytes, float v) {
 // Returns (through h1 / h2) the hit_triangle results up to that equivalence.
 template <bool LDS>
 __device__ __forceinline__ void leaf_pair_tests(const SceneView& S, bool at, int s0, float4 q3a, float4 q3b,
-                                                f3 o, f3 d, float t, float& h1, float& h2) {
+                                                f3 o, f3 d, float t, int max_pairs, float& h1, float& h2) {
     float ta = 0.0f, tb = 0.0f;
     if (at) {
         ta = tri_plane<LDS>(S, s0, q3a, o, d);
@@ -691,7 +692,7 @@ __device__ __forceinline__ void leaf_pair_tests(const SceneView& S, bool at, int
     const unsigned long long ma = __ballot(na), mb = __ballot(nb);
     const int ca = __popcll(ma), n = ca + __popcll(mb);
     bool oka = false, okb = false;
-    if (n <= 63) {
+    if (n <= max_pairs) {      // max_pairs <= 63 (tuning key 7; 0 = every lane tests its own)
         const int lane = lane_id();
         const int ja = rank_in(ma), jb = ca + rank_in(mb);
         // forward permutes hand worker j its pair's hit point o + d*t and slot; lanes
@@ -1397,7 +1398,7 @@ __global__ __launch_bounds__(256, MINW) void k_render_sm(KParams p) {
                 }
             } else {
 #if PT_LEAF_COMPACT
-                leaf_pair_tests<LDS>(S, at, s0, q3, at ? tri_quad<LDS>(S, s0 + 1, 3) : q3, o, d, t, h1, h2);
+                leaf_pair_tests<LDS>(S, at, s0, q3, at ? tri_quad<LDS>(S, s0 + 1, 3) : q3, o, d, t, p.compact_max, h1, h2);
 #else
                 if (at) {
                     f3 n0, n1;
@@ -1521,7 +1522,7 @@ struct pt_ctx {
     // 16/24 when the walk reads global memory (re-swept after the leaf compaction: +2% on
     // the C3 stand-in, +3% on C4 over 16/32); walk floor 8 / 6
     // (+0.8% on C2, +0.5% on C3 over no floor) -- tools/probe.py sweeps
-    int leaf_thresh = 0, shade_thresh = 0, minw = 0, trav_floor = 0;
+    int leaf_thresh = 0, shade_thresh = 0, minw = 0, trav_floor = 0, compact_max = 63;
     // frame-split work items (KParams::group): 0 = automatic, n = frames per item
     int group_force = 0;
     int n_cu = 0;
@@ -1871,6 +1872,12 @@ int pt_set_tuning(pt_ctx* c, int key, int value) {
         drop_graph(c);
         return PT_OK;
     }
+    if (key == 7) {
+        if (value < 0 || value > 63) return fail(c, PT_E_ARG, "compaction limit must be in 0..63");
+        c->compact_max = value;
+        drop_graph(c);
+        return PT_OK;
+    }
     if (value < 0 || value > 64) return fail(c, PT_E_ARG, "threshold must be in 1..64 (0 = automatic)");
     if (key == 0) c->leaf_thresh = value;
     else if (key == 1) c->shade_thresh = value;
@@ -1971,6 +1978,7 @@ static int enqueue_render(pt_ctx* c, int frame_first, int n_frames, int acc_firs
         p.leaf_thresh = c->leaf_thresh ? c->leaf_thresh : (lds_scene ? 52 : 16);
         p.shade_thresh = c->shade_thresh ? c->shade_thresh : (lds_scene ? 44 : 24);
         p.trav_floor = c->trav_floor ? c->trav_floor : (lds_scene ? 8 : 6);
+        p.compact_max = c->compact_max;
     }
     p.rW = 1.0f / (float)p.W;
     p.fW = (float)p.W;

@@ -280,7 +280,7 @@ class PathTracer:
         self._check(lib().pt_set_kernel(self.h, int(variant)))
 
     def set_tuning(self, leaf_thresh=None, shade_thresh=None, adaptive=None, waves_per_simd=None, group=None,
-                   trav_floor=None):
+                   trav_floor=None, compact_max=None):
         if leaf_thresh is not None:
             self._check(lib().pt_set_tuning(self.h, 0, int(leaf_thresh)))
         if shade_thresh is not None:
@@ -293,6 +293,8 @@ class PathTracer:
             self._check(lib().pt_set_tuning(self.h, 5, int(group)))
         if trav_floor is not None:
             self._check(lib().pt_set_tuning(self.h, 6, int(trav_floor)))
+        if compact_max is not None:
+            self._check(lib().pt_set_tuning(self.h, 7, int(compact_max)))
 
     def dispatch(self, frame, accumulate):
         """One glDispatchCompute with uniforms frame/accumulate (ogl_path_trace.h:176-183)."""

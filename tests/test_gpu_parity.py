@@ -260,6 +260,24 @@ def test_occupancy_builds_bitwise(cornell_scene, waves, variant, rpp):
                                                                                   floor))
 
 
+@pytest.mark.parametrize("compact_max", [0, 8, 63])
+@pytest.mark.parametrize("variant", [0, 3])
+def test_leaf_compaction_limits_bitwise(cornell_scene, compact_max, variant):
+    """Leaf-phase edge tests packed over the wave (tuning key 7): never (0), only for small
+    pair counts (8: most phases take the per-lane path), and up to 63 pairs (the default),
+    with leaf phases of up to 64 lanes (leaf threshold 64): the same bits each way."""
+    want = O.render(cornell_scene, 64, 40, max_bounce=8, n_frames=4)
+    for leaf in (0, 64):
+        pt = H.PathTracer(64, 40, max_bounce=8)
+        pt.set_kernel(variant)
+        pt.set_tuning(leaf, 0, compact_max=compact_max)
+        pt.upload(cornell_scene)
+        pt.render(1, 4, 0)
+        got = pt.read_rgba32f()
+        pt.close()
+        assert_bitwise(got, want, "compaction limit %d, leaf threshold %d" % (compact_max, leaf))
+
+
 def test_aces_epilogue(cornell_scene):
     pt = H.PathTracer(64, 64, max_bounce=5)
     pt.upload(cornell_scene)
