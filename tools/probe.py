@@ -42,7 +42,7 @@ def main():
     ap.add_argument("--width", type=int, default=1920)
     ap.add_argument("--height", type=int, default=1080)
     ap.add_argument("--bounces", type=int, default=8)
-    ap.add_argument("--tunings", default="0:0", help="leaf:shade[:adaptive[:waves[:group[:floor]]]] for variants 0/3, comma list")
+    ap.add_argument("--tunings", default="0:0", help="leaf:shade[:adaptive[:waves[:group[:floor[:compact]]]]] for variants 0/3, comma list")
     ap.add_argument("--world", type=int, default=1, help="render rank 0 of a WORLD-way row split (per-GPU share)")
     ap.add_argument("--flags", type=int, default=0, help="PT_FLAG_* bits (32 = Moller-Trumbore mode)")
     a = ap.parse_args()
@@ -58,7 +58,7 @@ def main():
             parts = [int(x) for x in tu.split(":")]
             pt.set_tuning(parts[0], parts[1], parts[2] if len(parts) > 2 else 1,
                           parts[3] if len(parts) > 3 else 0, parts[4] if len(parts) > 4 else None,
-                          parts[5] if len(parts) > 5 else None)
+                          parts[5] if len(parts) > 5 else None, parts[6] if len(parts) > 6 else None)
 
     for v, c, tu in configs:
         apply(v, tu)
