@@ -433,7 +433,10 @@ extern __shared__ float4 g_lds[];   // the state-machine kernel's scene copy (no
 // the hi half of a node sits at the compile-time offset 16 * kPadNodes from its lo half (an
 // immediate ds_read_b128 offset instead of an address add per walk step).  67: consecutive
 // images start 134 16-B granules apart, 6 mod 16, spreading them over the LDS bank groups.
-constexpr int kPadNodes = 67;
+#ifndef PT_PAD_NODES
+#define PT_PAD_NODES 67
+#endif
+constexpr int kPadNodes = PT_PAD_NODES;
 typedef float v4f __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) const v4f lds_v4f;
 template <bool LDS, bool PADN = false>
