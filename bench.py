@@ -33,7 +33,7 @@ HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
 
 # scene, W, H, spp, bounces, frames per launch, graph launches/replay
 CONFIGS = {
-    "C2": ("cornell", 1920, 1080, 1024, 8, 128, 0),
+    "C2": ("cornell", 1920, 1080, 1024, 8, 1024, 0),
     "C3": ("bunny", 1920, 1080, 256, 8, 256, 0),
     "C4": ("sponza", 1920, 1080, 256, 8, 256, 0),
     "C5": ("cornell", 3840, 2160, 4096, 8, 64, 8),
@@ -81,9 +81,10 @@ def main():
     bounces = args.bounces if args.bounces is not None else bounces
     world = int(os.environ.get("WORLD_SIZE", "1"))
     # frames per launch: the per-GPU share of the image shrinks with N, so launches get
-    # N times more frames (one launch tail per launch; measured: a 1080p/8 share runs at the
-    # single-GPU rate with 1024-frame launches, 13% slower with 128).  The graph config
-    # (C5) keeps its captured launch shape.
+    # N times more frames, capped at spp (one launch tail per launch; measured: C2 on one
+    # GPU runs 2.5% faster as one 1024-frame launch than as 8 of 128, and a 1080p/8 share
+    # runs at the single-GPU rate with 1024-frame launches, 13% slower with 128).  The graph
+    # config (C5) keeps its captured launch shape.
     if args.chunk:
         chunk = args.chunk
     elif graph_launches == 0:

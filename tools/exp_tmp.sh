@@ -1,3 +1,2 @@
 cd "$GRAFT_REPO_ROOT"; mkdir -p gpurun_out
-timeout -k 10 600 python tools/ab_inproc.py --libs cur,${EXP_LIBS} --rounds 4 > gpurun_out/ab_c2.log 2>&1 || exit $?
-echo "C2:"; grep median gpurun_out/ab_c2.log
+timeout -k 10 900 python tools/probe.py --spp 1024 --variants 0 --chunks 128,256,512,1024 --rounds 2 > gpurun_out/sweep.log 2>&1; echo "rc=$?"; grep "^round 1" gpurun_out/sweep.log | cut -c1-120

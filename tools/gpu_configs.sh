@@ -7,6 +7,6 @@ for c in C3 C4 C5; do
   echo "$c $(python3 -c "import json;d=json.load(open('$O/$c.json'));print(d['value'],d['ms_per_frame'])")"
 done
 for w in 2 4 8; do
-  timeout -k 10 600 python tools/probe.py --world $w --spp 1024 --variants 0 --chunks $((128*w)) --rounds 2 > "$O/w$w.log" 2>&1 || exit $?
+  timeout -k 10 600 python tools/probe.py --world $w --spp 1024 --variants 0 --chunks 1024 --rounds 2 > "$O/w$w.log" 2>&1 || exit $?
   echo "world $w: $(grep '^round 1' "$O/w$w.log" | cut -c1-90)"
 done

@@ -4,7 +4,7 @@
 cd "$GRAFT_REPO_ROOT"; R="$GRAFT_REPO_ROOT"; OUT="$R/gpurun_out/pmc"; mkdir -p "$OUT"
 export TMPDIR=/tmp
 cd /tmp
-ARGS=${PMC_ARGS:-"--chunk 128 --launches 2"}
+ARGS=${PMC_ARGS:-"--chunk 1024 --launches 2"}
 run() {  # name counters...
   local name=$1; shift
   timeout -k 10 300 rocprofv3 --kernel-trace --pmc "$@" --output-format csv -d "$OUT/$name" -o run -- \

@@ -45,7 +45,7 @@ def load(d):
 def main():
     pmc = sys.argv[1] if len(sys.argv) > 1 else os.path.join(REPO, "gpurun_out", "pmc")
     tag = sys.argv[2] if len(sys.argv) > 2 else "latest"
-    meta = dict(scene="cornell", width=1920, height=1080, chunk=128)
+    meta = dict(scene="cornell", width=1920, height=1080, chunk=1024)
     for a in sys.argv[3:]:
         k, v = a.split("=")
         meta[k] = int(v) if v.isdigit() else v
