@@ -36,7 +36,7 @@ CONFIGS = {
     "C2": ("cornell", 1920, 1080, 1024, 8, 1024, 0),
     "C3": ("bunny", 1920, 1080, 256, 8, 256, 0),
     "C4": ("sponza", 1920, 1080, 256, 8, 256, 0),
-    "C5": ("cornell", 3840, 2160, 4096, 8, 64, 8),
+    "C5": ("cornell", 3840, 2160, 4096, 8, 256, 8),     # 2 replays of 8 x 256 frames
 }
 
 

@@ -1,2 +1,5 @@
 cd "$GRAFT_REPO_ROOT"; mkdir -p gpurun_out
-timeout -k 10 900 python tools/probe.py --spp 1024 --variants 0 --chunks 128,256,512,1024 --rounds 2 > gpurun_out/sweep.log 2>&1; echo "rc=$?"; grep "^round 1" gpurun_out/sweep.log | cut -c1-120
+for c in 64 128 256 512; do
+  timeout -k 10 300 python bench.py --config C5 --chunk $c --no-cpu-baseline --steps 2 > gpurun_out/c5_$c.json 2> gpurun_out/c5_$c.err || exit $?
+  python3 -c "import json;d=json.load(open('gpurun_out/c5_$c.json'));print($c, d['value'], d['ms_per_frame'], d['config']['workload'][-30:])"
+done
