@@ -683,13 +683,17 @@ __device__ __forceinline__ float fperm_f(int dst_bytes, float v) {
 // test runs the same operations on the same values as at its source lane: the same bits.
 // Returns (through h1 / h2) the hit_triangle results up to that equivalence.
 template <bool LDS>
-__device__ __forceinline__ void leaf_pair_tests(const SceneView& S, bool at, int s0, float4 q3a, float4 q3b,
+__device__ __forceinline__ void leaf_pair_tests(const SceneView& S, bool at, int s0, float4 q3a,
                                                 f3 o, f3 d, float t, int max_pairs, float& h1, float& h2) {
     float ta = 0.0f, tb = 0.0f;
-    if (at) {
-        ta = tri_plane<LDS>(S, s0, q3a, o, d);
-        tb = tri_plane<LDS>(S, s0 + 1, q3b, o, d);
+    if (at) ta = tri_plane<LDS>(S, s0, q3a, o, d);
+    // a coplanar pair (q3a.w != 0: bitwise equal n and d0) has the same plane distance, so
+    // the second one is only computed when some lane's leaf is not such a pair
+    const bool cop = q3a.w != 0.0f;
+    if (__any(at & !cop)) {
+        if (at & !cop) tb = tri_plane<LDS>(S, s0 + 1, tri_quad<LDS>(S, s0 + 1, 3), o, d);
     }
+    tb = cop ? ta : tb;
     const bool na = at & (ta > 0.0001f) & (ta < t);
     const bool nb = at & (tb >= 0.0001f) & (tb < t);
     const unsigned long long ma = __ballot(na), mb = __ballot(nb);
@@ -1401,7 +1405,7 @@ __global__ __launch_bounds__(256, MINW) void k_render_sm(KParams p) {
                 }
             } else {
 #if PT_LEAF_COMPACT
-                leaf_pair_tests<LDS>(S, at, s0, q3, at ? tri_quad<LDS>(S, s0 + 1, 3) : q3, o, d, t, p.compact_max, h1, h2);
+                leaf_pair_tests<LDS>(S, at, s0, q3, o, d, t, p.compact_max, h1, h2);
 #else
                 if (at) {
                     f3 n0, n1;
@@ -1734,6 +1738,19 @@ int pt_upload_scene(pt_ctx* c, const float* tris, int n_tris, const float* bvh, 
             int t0 = (int)nd[8], t1 = (int)nd[9];
             put_tri(&dt[8 * (size_t)s], t0);
             put_tri(&dt[8 * (size_t)s + 4], t1);
+            {   // coplanar pair: both triangles carry the same (n, d0) up to the sign of zero
+                // components (the two halves of an OBJ quad, a single-triangle leaf's copy),
+                // flagged in the first slot's quad 3 .w.  hit_triangle's plane distance
+                // -(dot(n,o) + d0) / dot(n,d) is then the same for both wherever it can pass
+                // the leaf's acceptance tests: a zero factor of either sign only changes the
+                // sign of zero intermediate sums, so the two quotients are bitwise equal or
+                // both +-0, +-inf or NaN, which fail t > 1e-4 / t >= 1e-4 alike.  NaN (a
+                // degenerate triangle) never compares equal: such pairs are not flagged.
+                const float4* A = &dt[8 * (size_t)s];
+                const float4* B = A + 4;
+                const bool cop = A[0].w == B[0].w && A[1].w == B[1].w && A[2].w == B[2].w && A[3].x == B[3].x;
+                dt[8 * (size_t)s + 3].w = cop ? 1.0f : 0.0f;
+            }
             a = ~((s << 1) | (t0 == t1 ? 1 : 0));
             b = (int)nd[11];
             slot_of[pos[i]] = s;
