@@ -677,9 +677,8 @@ __device__ __forceinline__ float fperm_f(int dst_bytes, float v) {
 // `h2 < 1e-4` and fail c2).  About 47% of the triangle tests of a Cornell frame need them
 // (81% with the plain t >= 0 cull: a bounce ray starts ON the surface it left, at a plane
 // distance near 0).  The wave's needed (lane, triangle) pairs are packed onto its first lanes
-// -- a forward permute hands each worker lane its source, backward permutes fetch o, d and
-// the plane distance -- so one pass of edge tests serves both triangles of every lane; a
-// ballot returns the verdicts.  More than 63 pairs: each lane tests its own.  Every edge
+// -- forward permutes hand each worker lane its pair's hit point o + d*t and slot -- so one
+// pass of edge tests serves both triangles of every lane; a ballot returns the verdicts.  More than 63 pairs: each lane tests its own.  Every edge
 // test runs the same operations on the same values as at its source lane: the same bits.
 // Returns (through h1 / h2) the hit_triangle results up to that equivalence.
 template <bool LDS>
@@ -687,7 +686,8 @@ __device__ __forceinline__ void leaf_pair_tests(const SceneView& S, bool at, int
                                                 f3 o, f3 d, float t, int max_pairs, float& h1, float& h2) {
     float ta = 0.0f, tb = 0.0f;
     if (at) ta = tri_plane<LDS>(S, s0, q3a, o, d);
-    // a coplanar pair (q3a.w != 0: bitwise equal n and d0) has the same plane distance, so
+    // a coplanar pair (q3a.w != 0: n and d0 equal up to the sign of zero components, flagged
+    // at upload) has the same plane distance wherever it can pass the acceptance tests, so
     // the second one is only computed when some lane's leaf is not such a pair
     const bool cop = q3a.w != 0.0f;
     if (__any(at & !cop)) {

@@ -1,7 +1,2 @@
 cd "$GRAFT_REPO_ROOT"; mkdir -p gpurun_out
-timeout -k 10 600 python -u -m pytest tests -q -m gpu -x --timeout 300 > gpurun_out/exp_tests.log 2>&1; rc=$?
-echo "pytest rc=$rc"; tail -2 gpurun_out/exp_tests.log; [ $rc -eq 0 ] || exit $rc
-timeout -k 10 400 python tools/ab_inproc.py --libs base,cur --rounds 3 > gpurun_out/ab_c2.log 2>&1 || exit $?
-echo "C2:"; grep median gpurun_out/ab_c2.log
-timeout -k 10 400 python tools/ab_inproc.py --libs base,cur --rounds 3 --scene bunny --spp 64 --chunk 64 > gpurun_out/ab_c3.log 2>&1 || exit $?
-echo "C3:"; grep median gpurun_out/ab_c3.log
+timeout -k 10 900 python tools/probe.py --spp 1024 --variants 0 --chunks 1024 --rounds 2 --tunings 52:44,48:44,44:44,56:44,48:40,52:48 > gpurun_out/sweep.log 2>&1; echo "rc=$?"; grep "^round 1" gpurun_out/sweep.log | cut -c1-80
