@@ -1,2 +1,5 @@
 cd "$GRAFT_REPO_ROOT"; mkdir -p gpurun_out
-timeout -k 10 900 python tools/probe.py --spp 1024 --variants 0 --chunks 1024 --rounds 2 --tunings 52:44,48:44,44:44,56:44,48:40,52:48 > gpurun_out/sweep.log 2>&1; echo "rc=$?"; grep "^round 1" gpurun_out/sweep.log | cut -c1-80
+timeout -k 10 600 python tools/ab_inproc.py --libs cur,u2,u6,u8 --rounds 3 --scene bunny --spp 64 --chunk 64 > gpurun_out/ab_c3.log 2>&1 || exit $?
+echo "C3:"; grep median gpurun_out/ab_c3.log
+timeout -k 10 600 python tools/ab_inproc.py --libs cur,u2,u6,u8 --rounds 3 --scene sponza --spp 32 --chunk 32 > gpurun_out/ab_c4.log 2>&1 || exit $?
+echo "C4:"; grep median gpurun_out/ab_c4.log
