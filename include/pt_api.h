@@ -70,7 +70,8 @@ int pt_set_camera(pt_ctx* ctx, const float cam[12]);
 
 /* Equivalent to n_frames reference dispatches with frame = frame_first .. frame_first+n-1;
  * only the first uses accumulate = accumulate_first, the rest accumulate = 1 (running
- * mean, computeShader.c:548-551).  Bit-identical to n_frames separate calls. */
+ * mean, computeShader.c:548-551).  Bit-identical to n_frames separate calls, for any
+ * n_frames: a render too large for one launch's scratch is split (tuning key 8). */
 int pt_render(pt_ctx* ctx, int frame_first, int n_frames, int accumulate_first);
 /* Same, enqueued on the context's stream without waiting (timing / overlap). */
 int pt_render_async(pt_ctx* ctx, int frame_first, int n_frames, int accumulate_first);
@@ -138,6 +139,10 @@ int pt_set_kernel(pt_ctx* ctx, int variant);
  * key 7 = leaf-phase compaction limit (0..63, default 63): the edge tests of a wave's leaf
  *         phase are packed onto its first lanes when at most this many (lane, triangle) pairs
  *         need them; 0 = every lane tests its own triangles.
+ * key 8 = frame-split scratch budget in MiB (0 = automatic: min(32 GiB, device memory / 4)).
+ *         A render whose per-frame colours (12 B per pixel-frame) exceed it -- or whose
+ *         32-bit work-queue ids would overflow -- runs as back-to-back launches, the first
+ *         with the caller's accumulate flag and the rest accumulating: the same image.
  * None of these change the image (each pixel's frames stay in order in one lane). */
 int pt_set_tuning(pt_ctx* ctx, int key, int value);
 

@@ -1535,6 +1535,13 @@ struct pt_ctx {
     int n_cu = 0;
     float* d_rgb = nullptr;        // per-(frame, pixel) colours of the frame-split mode
     size_t rgb_bytes = 0;
+    // frame-split scratch budget: a render needing more is issued as back-to-back launches
+    // (tuning key 8; default min(32 GiB, a quarter of the device memory))
+    size_t scratch_budget = 0;
+    // a captured graph bakes in the scratch pointer it was captured with: that buffer stays
+    // alive (owned here once ensure_rgb has moved on to a larger one) until drop_graph
+    float* graph_rgb = nullptr;
+    std::vector<float*> graph_owned;
     bool scene_ok = false, cam_ok = false, counting = false;
     float cam[12] = {0};
     int variant = 0;
@@ -1605,6 +1612,11 @@ int pt_create(const pt_config* cfg, pt_ctx** out) {
     HIPCHK(c, hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, cfg->device));
     c->persist_blocks = (unsigned)std::max(1, n_cu) * 8u;   // 8 x 256 threads = 32 waves per CU
     c->n_cu = std::max(1, n_cu);
+    {
+        size_t total_mem = 0;
+        HIPCHK(c, hipDeviceTotalMem(&total_mem, cfg->device));
+        c->scratch_budget = std::min<size_t>(32ull << 30, total_mem / 4);
+    }
     c->n_tiles = ((cfg->width + 7) / 8) * ((c->rows_local + 7) / 8);
     c->tiles_x = (cfg->width + 7) / 8;
     {
@@ -1623,6 +1635,7 @@ int pt_create(const pt_config* cfg, pt_ctx** out) {
 
 void pt_destroy(pt_ctx* c) {
     if (!c) return;
+    (void)hipSetDevice(c->cfg.device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     drop_graph(c);
     free_scene(c);
@@ -1809,6 +1822,7 @@ int pt_upload_scene(pt_ctx* c, const float* tris, int n_tris, const float* bvh, 
             if (leaf && k == 0) std::memcpy(&dt[8 * (size_t)slot_of[i] + 3].z, &hb, 4);
         }
     }
+    HIPCHK(c, hipStreamSynchronize(c->stream));   // a render in flight may still read the old scene
     drop_graph(c);
     free_scene(c);
     HIPCHK(c, hipMalloc(&c->d_walk_lds, dwl.size() * sizeof(float4)));
@@ -1871,6 +1885,9 @@ int pt_set_camera(pt_ctx* c, const float cam[12]) {
 
 int pt_set_counting(pt_ctx* c, int enable) {
     if (!c) return PT_E_ARG;
+    // graph replays never count (pt_progressive_setup refuses counting): a graph captured
+    // before counting was switched on would silently produce no counts, so it is dropped
+    if ((enable != 0) != c->counting) drop_graph(c);
     c->counting = enable != 0;
     return PT_OK;
 }
@@ -1886,6 +1903,18 @@ int pt_set_kernel(pt_ctx* c, int variant) {
 
 int pt_set_tuning(pt_ctx* c, int key, int value) {
     if (!c) return PT_E_ARG;
+    if (key == 8) {
+        if (value < 0) return fail(c, PT_E_ARG, "scratch budget (MiB) must be >= 0 (0 = automatic)");
+        if (value == 0) {
+            size_t total_mem = 0;
+            HIPCHK(c, hipDeviceTotalMem(&total_mem, c->cfg.device));
+            c->scratch_budget = std::min<size_t>(32ull << 30, total_mem / 4);
+        } else {
+            c->scratch_budget = (size_t)value << 20;
+        }
+        drop_graph(c);
+        return PT_OK;
+    }
     if (key == 5) {
         if (value < 0) return fail(c, PT_E_ARG, "frames per work item must be >= 1 (0 = automatic)");
         c->group_force = value;
@@ -1911,6 +1940,8 @@ int pt_set_tuning(pt_ctx* c, int key, int value) {
         if (!c->adaptive && c->n_tiles > 0) {       // back to raster order
             std::vector<unsigned> ident(c->n_tiles);
             for (int i = 0; i < c->n_tiles; i++) ident[i] = pack_tile(c, (unsigned)i);
+            HIPCHK(c, hipSetDevice(c->cfg.device));
+            HIPCHK(c, hipStreamSynchronize(c->stream));
             HIPCHK(c, hipMemcpy(c->d_tile_perm, ident.data(), ident.size() * sizeof(unsigned), hipMemcpyHostToDevice));
             c->cost_pending = false;
         }
@@ -1942,10 +1973,15 @@ static int plan_group(const pt_ctx* c, int n_frames) {
     return std::min(g, n_frames);
 }
 
+// Grows the frame-split scratch to n_frames frame planes.  Earlier launches on the stream may
+// still read the old buffer, so the stream is drained first; a buffer a captured graph was
+// built with is handed to the graph (freed by drop_graph) instead of being freed under it.
 static int ensure_rgb(pt_ctx* c, int n_frames) {
     size_t need = (size_t)std::max(c->rows_local, 1) * (size_t)c->cfg.width * (size_t)n_frames * 3 * sizeof(float);
     if (need <= c->rgb_bytes) return PT_OK;
-    (void)hipFree(c->d_rgb);
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    if (c->d_rgb && c->graph_exec && c->d_rgb == c->graph_rgb) c->graph_owned.push_back(c->d_rgb);
+    else (void)hipFree(c->d_rgb);
     c->d_rgb = nullptr;
     c->rgb_bytes = 0;
     HIPCHK(c, hipMalloc(&c->d_rgb, need));
@@ -1953,10 +1989,34 @@ static int ensure_rgb(pt_ctx* c, int n_frames) {
     return PT_OK;
 }
 
+// Queue ids are 32-bit: a launch's items * 64 plus what the resident waves can reserve past
+// the end (each wave pulls at most 64 ids, twice after the queue ran dry) stay below 2^32.
+constexpr unsigned long long kIdLimit = (1ull << 32) - (1ull << 24);
+
+// Frames of one launch for a render of n_frames: the largest count whose frame-split scratch
+// (12 B per pixel-frame) fits the context's budget and whose queue ids stay 32-bit.  A longer
+// render is issued as back-to-back launches of at most this many frames; only the first one
+// uses the caller's accumulate flag, so the result is that of n_frames dispatches (pt_api.h).
+static int launch_frames(const pt_ctx* c, int n_frames) {
+    const unsigned long long px = (unsigned long long)std::max(c->rows_local, 1) * (unsigned long long)c->cfg.width;
+    const unsigned long long tiles64 = (unsigned long long)std::max(c->n_tiles, 1) * 64ull;
+    int n = n_frames;
+    for (;;) {
+        const int g = plan_group(c, n);
+        if (g >= n) return n;                       // register mode: no scratch, one group
+        const unsigned long long by_budget = c->scratch_budget / (px * 12ull);
+        const unsigned long long ng = (unsigned long long)((n + g - 1) / g);
+        const unsigned long long by_ids = (kIdLimit / tiles64) * (unsigned long long)g;
+        if ((unsigned long long)n <= by_budget && ng * tiles64 < kIdLimit) return n;
+        const unsigned long long m = std::min<unsigned long long>({(unsigned long long)n - 1, by_budget, by_ids});
+        n = (int)std::max<unsigned long long>(m, 1ull);
+    }
+}
+
 // Enqueues one render launch (work-queue reset + kernel) on the context stream.  With
 // `frame_dev` the frame range is read on the device (progressive graph replay).
 static int enqueue_render(pt_ctx* c, int frame_first, int n_frames, int acc_first, const int* frame_dev,
-                          int frame_offset, bool events) {
+                          int frame_offset) {
     KParams p;
     std::memset(&p, 0, sizeof(p));
     p.sc.nodes = c->d_nodes;
@@ -2019,25 +2079,11 @@ static int enqueue_render(pt_ctx* c, int frame_first, int n_frames, int acc_firs
     p.tile_perm = c->d_tile_perm;
     p.tile_cost = (c->adaptive && !c->counting) ? c->d_tile_cost : nullptr;
     if (p.tile_cost) c->cost_pending = true;
-    if (c->counting) HIPCHK(c, hipMemsetAsync(c->d_counters, 0, 16 * sizeof(unsigned long long), c->stream));
     if (c->rows_local == 0) return PT_OK;
     // variants: 0 state-machine persistent (default), 1 one-lane-per-pixel tiles,
     // 2 while-while persistent, 3 = 0 with the scene forced to stay in global memory
     bool use_lds = (c->variant == 0 || c->variant == 2) && c->lds_bytes <= kLdsSceneMax;
     if (c->variant != 1) HIPCHK(c, hipMemsetAsync(c->d_work, 0, sizeof(unsigned), c->stream));
-    hipEvent_t ev[2] = {nullptr, nullptr};
-    if (events) {
-        for (int i = 0; i < 2; i++) {
-            if (c->ev_free.empty()) {
-                HIPCHK(c, hipEventCreate(&ev[i]));
-            } else {
-                ev[i] = c->ev_free.back();
-                c->ev_free.pop_back();
-            }
-        }
-        c->ev_pending.emplace_back(ev[0], ev[1]);
-        HIPCHK(c, hipEventRecord(ev[0], c->stream));
-    }
     if (c->variant == 1) {
         dim3 grid((p.W + 15) / 16, (c->rows_local + 15) / 16);
         if (c->counting)
@@ -2091,8 +2137,34 @@ static int enqueue_render(pt_ctx* c, int frame_first, int n_frames, int acc_firs
         }
     }
     HIPCHK(c, hipGetLastError());
-    if (events) HIPCHK(c, hipEventRecord(ev[1], c->stream));
-    c->count_pending = c->counting;
+    return PT_OK;
+}
+
+// A pair of timing events from the recycled pool, queued for pt_sync.
+static int take_events(pt_ctx* c, hipEvent_t ev[2]) {
+    for (int i = 0; i < 2; i++) {
+        if (c->ev_free.empty()) {
+            HIPCHK(c, hipEventCreate(&ev[i]));
+        } else {
+            ev[i] = c->ev_free.back();
+            c->ev_free.pop_back();
+        }
+    }
+    c->ev_pending.emplace_back(ev[0], ev[1]);
+    return PT_OK;
+}
+
+// Enqueues a render of n_frames as launches of at most launch_frames() frames (one launch
+// when the scratch budget and the 32-bit queue ids allow).  Launch j > 0 continues the
+// running mean (accumulate = 1), so the image is that of n_frames single dispatches.
+static int enqueue_frames(pt_ctx* c, int frame_first, int n_frames, int acc_first, const int* frame_dev,
+                          int frame_offset) {
+    const int step = launch_frames(c, n_frames);
+    for (int done = 0; done < n_frames; done += step) {
+        const int n = std::min(step, n_frames - done);
+        int rc = enqueue_render(c, frame_first + done, n, done ? 1 : acc_first, frame_dev, frame_offset + done);
+        if (rc) return rc;
+    }
     return PT_OK;
 }
 
@@ -2101,7 +2173,16 @@ int pt_render_async(pt_ctx* c, int frame_first, int n_frames, int acc_first) {
     if (!c->scene_ok) return fail(c, PT_E_STATE, "pt_render before pt_upload_scene");
     if (n_frames <= 0) return fail(c, PT_E_ARG, "n_frames must be > 0");
     HIPCHK(c, hipSetDevice(c->cfg.device));
-    return enqueue_render(c, frame_first, n_frames, acc_first, nullptr, 0, true);
+    if (c->counting) HIPCHK(c, hipMemsetAsync(c->d_counters, 0, 16 * sizeof(unsigned long long), c->stream));
+    hipEvent_t ev[2];
+    int rc = take_events(c, ev);
+    if (rc) return rc;
+    HIPCHK(c, hipEventRecord(ev[0], c->stream));
+    rc = enqueue_frames(c, frame_first, n_frames, acc_first, nullptr, 0);
+    if (rc) return rc;
+    HIPCHK(c, hipEventRecord(ev[1], c->stream));
+    c->count_pending = c->counting;
+    return PT_OK;
 }
 
 static void drop_graph(pt_ctx* c) {
@@ -2109,6 +2190,13 @@ static void drop_graph(pt_ctx* c) {
     if (c->graph) (void)hipGraphDestroy(c->graph);
     c->graph_exec = nullptr;
     c->graph = nullptr;
+    c->graph_rgb = nullptr;
+    if (!c->graph_owned.empty()) {      // scratch only the dropped graph still referenced
+        (void)hipSetDevice(c->cfg.device);
+        (void)hipStreamSynchronize(c->stream);
+        for (float* b : c->graph_owned) (void)hipFree(b);
+        c->graph_owned.clear();
+    }
 }
 
 int pt_progressive_setup(pt_ctx* c, int frames_per_launch, int launches_per_replay) {
@@ -2120,14 +2208,17 @@ int pt_progressive_setup(pt_ctx* c, int frames_per_launch, int launches_per_repl
     HIPCHK(c, hipStreamSynchronize(c->stream));
     drop_graph(c);
     if (!c->d_frame) HIPCHK(c, hipMalloc(&c->d_frame, 64));
-    if (plan_group(c, frames_per_launch) < frames_per_launch) {   // no allocation inside the capture
-        int rc0 = ensure_rgb(c, frames_per_launch);
-        if (rc0) return rc0;
+    {   // no allocation inside the capture: the scratch of the largest sub-launch first
+        const int n = launch_frames(c, frames_per_launch);
+        if (plan_group(c, n) < n) {
+            int rc0 = ensure_rgb(c, n);
+            if (rc0) return rc0;
+        }
     }
     HIPCHK(c, hipStreamBeginCapture(c->stream, hipStreamCaptureModeThreadLocal));
     int rc = PT_OK;
     for (int i = 0; i < launches_per_replay && rc == PT_OK; i++)
-        rc = enqueue_render(c, 0, frames_per_launch, 0, c->d_frame, i * frames_per_launch, false);
+        rc = enqueue_frames(c, 0, frames_per_launch, 0, c->d_frame, i * frames_per_launch);
     if (rc == PT_OK) {
         hipLaunchKernelGGL(k_advance_frames, dim3(1), dim3(64), 0, c->stream, c->d_frame,
                            frames_per_launch * launches_per_replay);
@@ -2138,6 +2229,7 @@ int pt_progressive_setup(pt_ctx* c, int frames_per_launch, int launches_per_repl
     if (e != hipSuccess) return fail(c, PT_E_HIP, std::string("hipStreamEndCapture: ") + hipGetErrorString(e));
     c->graph = g;
     HIPCHK(c, hipGraphInstantiate(&c->graph_exec, g, nullptr, nullptr, 0));
+    c->graph_rgb = c->d_rgb;
     c->graph_frames = frames_per_launch * launches_per_replay;
     return pt_progressive_reset(c, 1);
 }
@@ -2146,6 +2238,7 @@ int pt_progressive_reset(pt_ctx* c, int next_frame) {
     if (!c) return PT_E_ARG;
     if (!c->d_frame) return fail(c, PT_E_STATE, "pt_progressive_setup first");
     if (next_frame < 1) return fail(c, PT_E_ARG, "frames start at 1");
+    HIPCHK(c, hipSetDevice(c->cfg.device));
     HIPCHK(c, hipMemcpyAsync(c->d_frame, &next_frame, sizeof(int), hipMemcpyHostToDevice, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
     return PT_OK;
@@ -2175,6 +2268,7 @@ int pt_progressive_run(pt_ctx* c, int replays) {
 
 int pt_sync(pt_ctx* c) {
     if (!c) return PT_E_ARG;
+    HIPCHK(c, hipSetDevice(c->cfg.device));
     HIPCHK(c, hipStreamSynchronize(c->stream));
     for (auto& pr : c->ev_pending) {
         float ms = 0;
@@ -2228,6 +2322,7 @@ int pt_read_rgba32f(pt_ctx* c, float* dst, size_t bytes) {
     if (!c || !dst) return PT_E_ARG;
     size_t need = (size_t)c->rows_local * c->cfg.width * sizeof(float4);
     if (bytes < need) return fail(c, PT_E_ARG, "destination too small");
+    HIPCHK(c, hipSetDevice(c->cfg.device));
     HIPCHK(c, hipStreamSynchronize(c->stream));
     HIPCHK(c, hipMemcpy(dst, c->accum, need, hipMemcpyDeviceToHost));
     return PT_OK;
@@ -2237,6 +2332,7 @@ int pt_write_rgba32f(pt_ctx* c, const float* src, size_t bytes) {
     if (!c || !src) return PT_E_ARG;
     size_t need = (size_t)c->rows_local * c->cfg.width * sizeof(float4);
     if (bytes < need) return fail(c, PT_E_ARG, "source too small");
+    HIPCHK(c, hipSetDevice(c->cfg.device));
     HIPCHK(c, hipStreamSynchronize(c->stream));
     HIPCHK(c, hipMemcpy(c->accum, src, need, hipMemcpyHostToDevice));
     return PT_OK;
@@ -2247,6 +2343,7 @@ int pt_read_rgba8_aces(pt_ctx* c, unsigned char* dst, size_t bytes) {
     long long n = (long long)c->rows_local * c->cfg.width;
     if (bytes < (size_t)n * 4) return fail(c, PT_E_ARG, "destination too small");
     if (n == 0) return PT_OK;
+    HIPCHK(c, hipSetDevice(c->cfg.device));
     hipLaunchKernelGGL(k_aces, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, c->stream, c->accum, c->rgba8, n);
     HIPCHK(c, hipGetLastError());
     HIPCHK(c, hipStreamSynchronize(c->stream));
@@ -2265,6 +2362,7 @@ int pt_copy_rows_device(pt_ctx* c, void* dst, size_t bytes) {
     if (!c || !dst) return PT_E_ARG;
     size_t need = (size_t)c->rows_local * c->cfg.width * sizeof(float4);
     if (bytes < need) return fail(c, PT_E_ARG, "destination too small");
+    HIPCHK(c, hipSetDevice(c->cfg.device));
     HIPCHK(c, hipMemcpyAsync(dst, c->accum, need, hipMemcpyDeviceToDevice, c->stream));
     return pt_sync(c);
 }

@@ -280,7 +280,7 @@ class PathTracer:
         self._check(lib().pt_set_kernel(self.h, int(variant)))
 
     def set_tuning(self, leaf_thresh=None, shade_thresh=None, adaptive=None, waves_per_simd=None, group=None,
-                   trav_floor=None, compact_max=None):
+                   trav_floor=None, compact_max=None, scratch_mib=None):
         if leaf_thresh is not None:
             self._check(lib().pt_set_tuning(self.h, 0, int(leaf_thresh)))
         if shade_thresh is not None:
@@ -295,6 +295,8 @@ class PathTracer:
             self._check(lib().pt_set_tuning(self.h, 6, int(trav_floor)))
         if compact_max is not None:
             self._check(lib().pt_set_tuning(self.h, 7, int(compact_max)))
+        if scratch_mib is not None:
+            self._check(lib().pt_set_tuning(self.h, 8, int(scratch_mib)))
 
     def dispatch(self, frame, accumulate):
         """One glDispatchCompute with uniforms frame/accumulate (ogl_path_trace.h:176-183)."""

@@ -1,0 +1,116 @@
+"""Context lifecycle on the GPU: scratch ownership across graph capture and later renders,
+renders split by the scratch budget and by the 32-bit queue-id range, counting vs graph
+replay, and one process driving contexts on two devices.  Every image check is bit-exact.
+"""
+import ctypes
+
+import numpy as np
+import pytest
+
+import oracle_lib as O
+import pt_host as H
+from test_gpu_parity import assert_bitwise
+
+pytestmark = pytest.mark.gpu
+
+
+def test_graph_survives_larger_render(cornell_scene):
+    """A graph captured with a small frame-split scratch must keep working after a later
+    pt_render grew (reallocated) the context's scratch: setup, larger render, replay."""
+    want = O.render(cornell_scene, 40, 24, max_bounce=8, n_frames=6)
+    pt = H.PathTracer(40, 24, max_bounce=8)
+    pt.set_tuning(group=1)                      # frame-split items in every launch
+    pt.upload(cornell_scene)
+    pt.progressive_setup(frames_per_launch=2, launches_per_replay=3)
+    pt.render(1, 12, 0)                         # needs 6x the scratch the graph holds
+    pt.progressive_reset(1)
+    pt.progressive_run(replays=1)
+    got = pt.read_rgba32f()
+    pt.render(1, 24, 0)                         # grows it again, then replays once more
+    pt.progressive_reset(1)
+    pt.progressive_run(replays=1)
+    got2 = pt.read_rgba32f()
+    pt.close()
+    assert_bitwise(got, want, "graph after a larger render")
+    assert_bitwise(got2, want, "graph after two larger renders")
+
+
+@pytest.mark.parametrize("variant", [0, 3])
+def test_scratch_budget_splits_render(cornell_scene, variant):
+    """A 1 MiB scratch budget holds 34 frames of a 64x40 image: a 100-frame render runs as
+    3 launches (accumulate continues across them), in direct and graph mode, with the
+    counting build's totals those of the oracle."""
+    want, cnt = O.render(cornell_scene, 64, 40, max_bounce=8, n_frames=100, counters=True)
+    pt = H.PathTracer(64, 40, max_bounce=8)
+    pt.set_kernel(variant)
+    pt.set_tuning(group=2, scratch_mib=1)
+    pt.upload(cornell_scene)
+    pt.set_counting(True)
+    pt.render(1, 100, 0)
+    st = pt.stats()[1]
+    got = pt.read_rgba32f()
+    pt.set_counting(False)
+    pt.progressive_setup(frames_per_launch=50, launches_per_replay=2)
+    pt.progressive_run(replays=1)
+    got_graph = pt.read_rgba32f()
+    pt.close()
+    assert_bitwise(got, want, "budget split")
+    assert_bitwise(got_graph, want, "budget split, graph")
+    assert [st["segments"], st["node_visits"], st["tri_tests"], st["sphere_tests"], st["hits"]] == \
+        [int(x) for x in cnt]
+
+
+def test_queue_ids_stay_32_bit(cornell_scene):
+    """1024x1024 with one frame per work item and 4096 frames is 2^32 queue ids: the render
+    must be split (it used to wrap and silently skip work).  Checked against the same
+    frames rendered as four 1024-frame launches (each far inside the id range)."""
+    W = Hh = 1024
+    pt = H.PathTracer(W, Hh, max_bounce=0, display_mode=2)
+    pt.set_tuning(group=1, scratch_mib=60000)  # the budget alone would allow one launch
+    pt.upload(cornell_scene)
+    pt.render(1, 4096, 0)
+    got = pt.read_rgba32f()
+    pt.set_tuning(scratch_mib=0)
+    for f0 in range(1, 4097, 1024):
+        pt.render(f0, 1024, 0 if f0 == 1 else 1)
+    want = pt.read_rgba32f()
+    pt.close()
+    assert np.all(np.isfinite(got[..., 3])) and np.all(got[..., 3] == np.float32(1.0))
+    assert_bitwise(got, want, "2^32 queue ids")
+
+
+def test_counting_after_graph_setup_refused(cornell_scene):
+    """Switching counting on after the capture drops the graph: a replay would count
+    nothing, so pt_progressive_run reports PT_E_STATE instead."""
+    pt = H.PathTracer(32, 16, max_bounce=4)
+    pt.upload(cornell_scene)
+    pt.progressive_setup(frames_per_launch=2, launches_per_replay=1)
+    pt.set_counting(True)
+    with pytest.raises(H.PTError) as e:
+        pt.progressive_run(replays=1)
+    assert e.value.code == -6
+    pt.close()
+
+
+def _device_count():
+    import torch
+    return torch.cuda.device_count()
+
+
+@pytest.mark.skipif("_device_count() < 2")
+def test_two_devices_one_process(cornell_scene):
+    """Contexts on devices 0 and 1 driven alternately from one thread: every entry point
+    selects its context's device (sync, readback, ACES, tuning)."""
+    want = O.render(cornell_scene, 48, 32, max_bounce=6, n_frames=3)
+    pts = [H.PathTracer(48, 32, max_bounce=6, device=d) for d in (0, 1)]
+    for pt in pts:
+        pt.upload(cornell_scene)
+    for pt in pts:
+        pt.render_async(1, 3, 0)
+    for pt in pts:
+        pt.sync()
+        pt.set_tuning(adaptive=0)
+        assert_bitwise(pt.read_rgba32f(), want, "device context")
+        assert np.array_equal(pt.read_rgba8(), O.aces_rgba8(want))
+    for pt in pts:
+        pt.close()
