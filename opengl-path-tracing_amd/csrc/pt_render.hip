@@ -78,6 +78,10 @@ struct KParams {
     // a leaf): a ray starting inside the root box hits it, so the walk may start at the child
     float root_box[6];
     int root_child;
+    // variant 4 (wavefront kernel): path slots per workgroup, the walker count at which a
+    // wave stops walking to refill, and the queue depths that start a leaf / shade batch
+    int wf_paths, wf_ring, wf_refill, wf_leaf_min, wf_shade_min;
+    unsigned* wf_err;              // watchdog trips of the wavefront kernel (must stay 0)
 };
 
 // Progressive mode (hipGraph replay): the frame range comes from a device counter, and
@@ -1470,6 +1474,577 @@ __global__ __launch_bounds__(256) void k_accum_frames(KParams p) {
     p.accum[idx] = acc;
 }
 
+// =====================================================================================
+// Variant 4: wavefront kernel with workgroup queues (LDS-staged scenes).
+//
+// The state-machine kernel ties a path to one lane for its whole life, so a wave walks,
+// leaf-tests or shades with only the lanes in that state (measured on C2: 44% / 70% / 73%
+// of the lanes).  Here the paths live in LDS records, one per path slot, and waves are
+// workers: a wave keeps up to 64 rays walking in registers and refills lanes from a walk
+// queue as rays stop; rays that stop at a hit leaf go to a leaf queue, rays whose walk ended
+// to a shade queue, and any wave takes batches of 64 from those queues (leaf tests / shading
+// + path regeneration), pushing the rays back to the walk queue.  Every path still runs the
+// reference's operations in the reference's order (node, its leaf's tests before the next
+// node, the same t; frames in order through the frame-colour buffer), so the image is the
+// same bits; only which lane executes which step changes.
+//
+// One workgroup of 16 waves per CU shares one scene copy and P path slots:
+//   ray record  (3 float4 planes): {o, t}, {d, hprim}, {rd, w}   (rd = 0: outside the guard)
+//   path record (3 float4 planes): {col, rng}, {inc, x | y << 16}, {pixel, k | kend << 16,
+//                                   bounce | flags << 8 | segments << 16, tile}
+//   queues: rings of (slot + 1) in u16, 0 = not yet written, with per-queue {tail, head,
+//   avail} counters; `avail` counts published entries, a pop reserves from it first.
+// =====================================================================================
+constexpr int kWfQW = 0, kWfQL = 1, kWfQS = 2; // walk, leaf, shade queues
+constexpr unsigned kWfChunk = 256;             // work ids a workgroup takes from the device queue at once
+constexpr int kWfLive = 9;                     // counter: path slots not yet retired
+constexpr unsigned kWfFresh = 1u, kWfNeedRay = 2u, kWfHasPx = 4u;
+
+#ifdef PT_WF_DIAG
+// experiment builds only (-DPT_WF_DIAG): per-wave counters of the wavefront kernel, read back
+// by pt_debug_wf_diag: [0] walk wave-steps, [1] walk lane-steps, [2] leaf batches, [3] leaf
+// lanes, [4] shade batches, [5] shade lanes, [6] idle sleeps, [7..10] clocks walk / leaf /
+// shade / idle, [11] refilled lanes, [12] pops that waited for an entry
+__device__ unsigned long long g_wf_diag[16];
+struct WfDiag {
+    unsigned long long v[16] = {};
+    __device__ void add(int i, unsigned long long x) { v[i] += x; }
+    __device__ void flush() {
+        if (lane_id() == 0)
+            for (int i = 0; i < 16; i++) atomicAdd(&g_wf_diag[i], v[i]);
+    }
+};
+#else
+struct WfDiag {
+    __device__ void add(int, unsigned long long) {}
+    __device__ void flush() {}
+};
+#endif
+#define WF_DIAG(i, v) dg.add(i, (unsigned long long)(v))
+typedef __attribute__((address_space(3))) unsigned lds_u32;
+typedef __attribute__((address_space(3))) unsigned short lds_u16;
+typedef __attribute__((address_space(3))) v4f lds_v4;
+
+struct WfLds {
+    int r0, r1, r2, q0, q1, q2;   // float4 plane bases
+    unsigned ring;                // byte offset of the 3 rings (rmask + 1 entries each)
+    unsigned rmask;
+    unsigned ctr;                 // byte offset of the counters
+};
+__device__ __forceinline__ v4f wf_ld(int plane, int s) { return *(lds_v4*)(size_t)(unsigned)((plane + s) << 4); }
+__device__ __forceinline__ void wf_st(int plane, int s, v4f v) { *(lds_v4*)(size_t)(unsigned)((plane + s) << 4) = v; }
+__device__ __forceinline__ void wf_stw(int plane, int s, float v) {   // .w only
+    *(__attribute__((address_space(3))) float*)(size_t)(unsigned)(((plane + s) << 4) + 12) = v;
+}
+__device__ __forceinline__ lds_u32* wf_ctr(const WfLds& L, int i) { return (lds_u32*)(size_t)(L.ctr + 4u * i); }
+__device__ __forceinline__ unsigned wf_peek(const WfLds& L, int i) {    // wave-uniform read
+    return (unsigned)__builtin_amdgcn_readfirstlane((int)*(volatile lds_u32*)wf_ctr(L, i));
+}
+
+// Pushes the slot of every lane with m set onto queue q (records written before the call).
+__device__ __forceinline__ void wf_push(const WfLds& L, int q, bool m, int slot) {
+    const unsigned long long b = __ballot(m);
+    if (!b) return;
+    const int n = __popcll(b), leader = __ffsll((long long)b) - 1;
+    const int lane = lane_id();
+    unsigned base = 0;
+    if (lane == leader) base = __hip_atomic_fetch_add(wf_ctr(L, 3 * q), (unsigned)n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    base = (unsigned)__builtin_amdgcn_readlane((int)base, leader);
+    if (m) {
+        const unsigned pos = (base + (unsigned)rank_in(b)) & L.rmask;
+        *(volatile lds_u16*)(size_t)(L.ring + 2u * ((unsigned)q * (L.rmask + 1u) + pos)) = (unsigned short)(slot + 1);
+    }
+    // the records and ring entries must be in LDS before the entries are published (the LDS
+    // executes one wave's operations in order; the barrier keeps the compiler from sinking the
+    // stores below the publishing atomic)
+#ifdef PT_WF_NOWAIT
+    asm volatile("" ::: "memory");
+#else
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#endif
+    if (lane == leader) __hip_atomic_fetch_add(wf_ctr(L, 3 * q + 2), (unsigned)n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
+// Pops up to popcount(want) published entries of queue q for the lanes in `want` (in lane
+// order); a lane that gets none returns -1.
+// `strict`: all popcount(want) entries or none.
+__device__ __forceinline__ int wf_pop(const WfLds& L, int q, unsigned long long want, unsigned* err, WfDiag& dg,
+                                     bool strict = false) {
+    const int n = __popcll(want);
+    if (!n) return -1;
+    const int leader = __ffsll((long long)want) - 1;
+    const int lane = lane_id();
+    int got = 0;
+    unsigned head = 0;
+    if (lane == leader) {
+        const int a = (int)__hip_atomic_fetch_add(wf_ctr(L, 3 * q + 2), (unsigned)-n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        got = a >= n ? n : (a > 0 && !strict ? a : 0);
+        if (got < n) __hip_atomic_fetch_add(wf_ctr(L, 3 * q + 2), (unsigned)(n - got), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        if (got) head = __hip_atomic_fetch_add(wf_ctr(L, 3 * q + 1), (unsigned)got, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    }
+    got = __builtin_amdgcn_readlane(got, leader);
+    head = (unsigned)__builtin_amdgcn_readlane((int)head, leader);
+    const int r = rank_in(want);
+    int slot = -1;
+    if (((want >> lane) & 1ull) && r < got) {
+        volatile lds_u16* e = (volatile lds_u16*)(size_t)(L.ring + 2u * ((unsigned)q * (L.rmask + 1u) + ((head + (unsigned)r) & L.rmask)));
+        unsigned v = *e;
+        if (v == 0u) {               // reserved by a producer that has not written it yet
+            WF_DIAG(12, 1);
+            const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+            while (v == 0u) {
+                __builtin_amdgcn_s_sleep(1);
+                v = *e;
+                // watchdog (100 MHz clock): a producer never takes 1 s to write its entry
+                if (v == 0u && __builtin_amdgcn_s_memrealtime() - t0 > 100000000ull) {
+                    atomicAdd(err, 1u);
+                    return -1;
+                }
+            }
+        }
+        *e = 0;
+        slot = (int)v - 1;
+    }
+    return slot;
+}
+
+// The walk of the wavefront kernel: the lanes with w >= 0 take node steps (bvh_intersect +
+// the link choice, WalkLinks) until at most `refill` of them still walk.
+template <bool ALL_FAST, bool PADN>
+__device__ __forceinline__ void wf_walk(const SceneView& S, f3 o, f3 d, f3 rd, bool fast, float t, int refill,
+                                        int& w, WfDiag& dg) {
+    for (;;) {
+#pragma unroll
+        for (int u = 0; u < kWalkUnroll; u++) {
+#ifdef PT_WF_DIAG
+            { const unsigned long long mm = __ballot(w >= 0); if (mm) { WF_DIAG(0, 1); WF_DIAG(1, __popcll(mm)); } }
+#endif
+            if (w >= 0) {
+                float4 lo, hi;
+                node_at<true, PADN>(S, w, lo, hi);
+                const int a = __float_as_int(hi.z), b = __float_as_int(hi.w);
+                const bool hb = (ALL_FAST || fast) ? slab_oct(lo, hi, o, d, rd, t) : slab(lo, hi, o, d, t);
+                w = hb ? a : b;
+            }
+        }
+        if (__popcll(__ballot(w >= 0)) <= refill) break;
+    }
+}
+
+// Leaf batch: up to 64 rays from the leaf queue, both triangle tests + the 2-way choice
+// (:406-429), then back to the walk queue at the leaf's continuation (or to the shade queue).
+__device__ __forceinline__ bool wf_leaf_batch(const KParams& p, const SceneView& S, const WfLds& L, WfDiag& dg,
+                                              bool strict) {
+    const int s = wf_pop(L, kWfQL, ~0ull, p.wf_err, dg, strict);
+    const bool at = s >= 0;
+    if (!__any(at)) return false;
+    WF_DIAG(2, 1);
+    WF_DIAG(3, __popcll(__ballot(at)));
+    const int si = at ? s : 0;
+    const v4f a0 = wf_ld(L.r0, si), a1 = wf_ld(L.r1, si), a2 = wf_ld(L.r2, si);
+    const f3 o = mk(a0.x, a0.y, a0.z), d = mk(a1.x, a1.y, a1.z);
+    float t = a0.w;
+    int hprim = __float_as_int(a1.w);
+    const bool fast = a2.x != 0.0f;
+    const int code = at ? -2 - __float_as_int(a2.w) : 0;    // (slot << 1) | single
+    const int s0 = code & ~1;
+    const float4 q3 = tri_quad<true>(S, s0, 3);
+    int cont = __float_as_int(q3.z);                          // next-right, image-0 offset
+    if (fast & (cont >= 0)) cont += oct_base(d, S.np << 5);
+    float h1 = -1.0f, h2 = -1.0f;
+    if (p.flags & PT_FLAG_MOLLER_TRUMBORE) {
+        if (at) {
+            h1 = tri_mt(tri_quad<true>(S, s0, 0), tri_quad<true>(S, s0, 1), tri_quad<true>(S, s0, 2), o, d);
+            h2 = tri_mt(tri_quad<true>(S, s0 + 1, 0), tri_quad<true>(S, s0 + 1, 1), tri_quad<true>(S, s0 + 1, 2), o, d);
+        }
+    } else {
+        leaf_pair_tests<true>(S, at, s0, q3, o, d, t, p.compact_max, h1, h2);
+    }
+    if (at) {
+        const bool c1 = (h1 > 0.0001f) & (h1 < t) & ((h1 < h2) | (h2 < 0.0001f));
+        const bool c2 = !c1 & (h2 > 0.0001f) & (h2 < t);
+        if (c1 | c2) {
+            t = c1 ? h1 : h2;
+            hprim = s0 + (c1 ? 0 : 1);
+            wf_stw(L.r0, s, t);
+            wf_stw(L.r1, s, __int_as_float(hprim));
+        }
+        wf_stw(L.r2, s, __int_as_float(cont));
+    }
+    wf_push(L, kWfQW, at & (cont >= 0), s);
+    wf_push(L, kWfQS, at & (cont < 0), s);
+    return true;
+}
+
+// Shade batch: up to 64 paths from the shade queue.  Finishes their segments (the body of
+// Trace's loop, :447-498), stores finished frames' colours, regenerates finished paths
+// (next frame of the work item, or a new item from the device queue), sets up the next
+// segment (guard, spheres :372-385, walk start) and queues it.  The operations are those of
+// k_render_sm's SHADE phase for one path.
+__device__ __forceinline__ bool wf_shade_batch(const KParams& p, const SceneView& S, const WfLds& L,
+                                               unsigned total_ids, unsigned n_groups, int root_skip, WfDiag& dg,
+                                               bool strict) {
+    const int s = wf_pop(L, kWfQS, ~0ull, p.wf_err, dg, strict);
+    bool act = s >= 0;
+    if (!__any(act)) return false;
+    WF_DIAG(4, 1);
+    WF_DIAG(5, __popcll(__ballot(act)));
+    const int si = act ? s : 0;
+    const v4f a0 = wf_ld(L.r0, si), a1 = wf_ld(L.r1, si);
+    const v4f b0 = wf_ld(L.q0, si), b1 = wf_ld(L.q1, si), b2 = wf_ld(L.q2, si);
+    f3 o = mk(a0.x, a0.y, a0.z), d = mk(a1.x, a1.y, a1.z);
+    float t = a0.w;
+    int hprim = __float_as_int(a1.w);
+    f3 col = mk(b0.x, b0.y, b0.z), inc = mk(b1.x, b1.y, b1.z);
+    uint32_t state = __float_as_uint(b0.w);
+    const unsigned lxy = __float_as_uint(b1.w);
+    int lx = (int)(lxy & 0xffffu), y = (int)(lxy >> 16);
+    int aidx = (int)__float_as_uint(b2.x);
+    int k = (int)(__float_as_uint(b2.y) & 0xffffu), kend = (int)(__float_as_uint(b2.y) >> 16);
+    const unsigned bfl = __float_as_uint(b2.z);
+    int bounce = (int)(bfl & 0xffu);
+    unsigned flags = (bfl >> 8) & 0xffu, pcost = bfl >> 16;
+    unsigned tile_id = __float_as_uint(b2.w);
+    bool need_ray = (flags & kWfNeedRay) != 0u, has_px = (flags & kWfHasPx) != 0u;
+
+    if (act && !(flags & kWfFresh)) {
+        const bool hit = hprim != -1;
+        pcost++;
+        bool finished = false;
+        f3 rgb = inc;
+        if (hit && pt::length_gt_001(col)) {
+            const f3 hitp = o + d * t;
+            f3 normal;
+            int mat;
+            if (hprim >= 0) {
+                normal = mk(tri_quad<true>(S, hprim, 0).w, tri_quad<true>(S, hprim, 1).w, tri_quad<true>(S, hprim, 2).w);
+                mat = __float_as_int(tri_quad<true>(S, hprim, 3).y);
+            } else {
+                const int sph = -2 - hprim;
+                const float4 c0 = S.spheres[2 * sph];
+                normal = pt::normalize(hitp - mk(c0.x, c0.y, c0.z));
+                mat = __float_as_int(S.spheres[2 * sph + 1].x);
+            }
+            if (pt::dot(normal, d) > 0.0f) normal = normal * -1.0f;
+            if (p.mode == 2) {
+                rgb = (normal + mk(1, 1, 1)) * 0.5f;
+                finished = true;
+            } else if (p.mode == 4) {
+                const float sd = pt::length(hitp - o);
+                const float dist = 1.0f - pt::fsqrt(sd + 1.0f) / (sd + 1.0f);
+                const float q = dist * dist;
+                rgb = mk(q, q, q);
+                finished = true;
+            } else {
+                o = hitp;
+                const f3 diffuse = pt::normalize(normal + pt::random_unit_vector(state));
+                const float kk = 2.0f * pt::dot(normal, d);
+                const f3 specular = pt::normalize(d - normal * kk);
+                const float4 m0 = S.mats[3 * mat], m1 = S.mats[3 * mat + 1], m2 = S.mats[3 * mat + 2];
+                if (p.mode == 3) {
+                    rgb = mk(m0.x, m0.y, m0.z);
+                    finished = true;
+                } else {
+                    const float is_spec = (m1.w > pt::random01(state)) ? 1.0f : 0.0f;
+                    d = pt::mix(diffuse, specular, m0.w * is_spec);
+                    inc = inc + mk(m1.x, m1.y, m1.z) * col;
+                    col = col * pt::mix(mk(m0.x, m0.y, m0.z), mk(m2.x, m2.y, m2.z), is_spec);
+                    bounce++;
+                    if (bounce > p.max_bounce) {
+                        rgb = inc;
+                        finished = true;
+                    }
+                }
+            }
+        } else {
+            f3 env = mk(0, 0, 0);
+            if (!(p.flags & PT_FLAG_NO_SKY)) {
+                const f3 dir = pt::normalize(d);
+                const float tt = 0.5f * (dir.z + 1.0f);
+                const float omt = 1.0f - tt;
+                env = mk(omt * 1.0f + tt * 0.5f, omt * 1.0f + tt * 0.7f, omt * 1.0f + tt * 1.0f);
+            }
+            rgb = inc + env * col;
+            finished = true;
+        }
+        need_ray = finished;
+        if (finished) {   // raysPerPixel == 1: pixel = (0 + rgb) / 1 (:541-546)
+            const f3 px = (mk(0, 0, 0) + rgb) / 1.0f;
+            nt_store3(p.rgb + 3 * ((size_t)k * (size_t)(p.rows_local * p.W) + (size_t)aidx), px);
+            k++;
+        }
+    }
+    flags = kWfFresh;          // the finished segment (if any) is consumed
+    if (act & need_ray & has_px & (k >= kend)) {      // work item done: release the pixel
+        if (p.tile_cost && tile_id != ~0u) atomicAdd(&p.tile_cost[tile_id], pcost);
+        has_px = false;
+    }
+    // wave-aggregated pull from the device work queue: exactly the ids this batch hands out
+    // (any wave may shade any slot, so a wave must not keep reserved ids for later)
+    const bool want = act & !has_px;
+    const unsigned long long m = __ballot(want);
+    if (m) {
+        const unsigned need = (unsigned)__popcll(m);
+        const unsigned rank = (unsigned)rank_in(m);
+        const int leader = __ffsll((long long)m) - 1;
+        // the workgroup's id pool (counters 10 = next id, 11 = ids left, 12 = lock): a device
+        // atomic only once per kWfChunk ids (its return is a long stall); the ids of one pull
+        // may come from the old pool and a fresh chunk
+        unsigned base0 = 0, take0 = 0, base1 = 0;
+        if (want && rank == 0u) {
+            unsigned expected = 0u;
+            while (!__hip_atomic_compare_exchange_strong(wf_ctr(L, 12), &expected, 1u, __ATOMIC_RELAXED,
+                                                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) {
+                expected = 0u;
+                __builtin_amdgcn_s_sleep(1);
+            }
+            unsigned nx = *(volatile lds_u32*)wf_ctr(L, 10), left = *(volatile lds_u32*)wf_ctr(L, 11);
+            take0 = min(need, left);
+            base0 = nx;
+            nx += take0;
+            left -= take0;
+            if (take0 < need) {
+                base1 = atomicAdd(p.work_counter, kWfChunk);
+                nx = base1 + (need - take0);
+                left = kWfChunk - (need - take0);
+            }
+            *(volatile lds_u32*)wf_ctr(L, 10) = nx;
+            *(volatile lds_u32*)wf_ctr(L, 11) = left;
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            *(volatile lds_u32*)wf_ctr(L, 12) = 0u;
+        }
+        base0 = (unsigned)__builtin_amdgcn_readlane((int)base0, leader);
+        take0 = (unsigned)__builtin_amdgcn_readlane((int)take0, leader);
+        base1 = (unsigned)__builtin_amdgcn_readlane((int)base1, leader);
+        const unsigned id = rank < take0 ? base0 + rank : base1 + (rank - take0);
+        if (want) {
+            if (id >= total_ids) {
+                act = false;       // queue exhausted: the slot retires
+                __hip_atomic_fetch_add(wf_ctr(L, kWfLive), (unsigned)-1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            } else {
+                const unsigned item = id >> 6, wl = id & 63u;
+                unsigned tile = p.grp_magic ? __umulhi(item, p.grp_magic) : item / n_groups;
+                const int g = (int)(item - tile * n_groups);
+                const int tiles_x = (p.W + 7) >> 3;
+                int tx, ty;
+                if (p.tile_perm) {
+                    const unsigned pk = p.tile_perm[tile];
+                    tx = (int)(pk & 0xffffu);
+                    ty = (int)(pk >> 16);
+                } else {
+                    tx = (int)(tile % (unsigned)tiles_x);
+                    ty = (int)(tile / (unsigned)tiles_x);
+                }
+                tile = (unsigned)(ty * tiles_x + tx);
+                const int cx = tx * 8 + (int)(wl & 7u), crow = ty * 8 + (int)(wl >> 3);
+                const int cy = p.row0 + crow * p.row_stride;
+                if ((cx < p.W) & (crow < p.rows_local) & (cx < p.x_limit) & (cy < p.y_limit)) {
+                    lx = cx;
+                    y = cy;
+                    aidx = crow * p.W + cx;
+                    tile_id = ((wl & 0x1bu) == 0u) ? tile : ~0u;
+                    pcost = 0;
+                    k = g * p.group;
+                    kend = min(k + p.group, p.n_frames);
+                    need_ray = true;
+                    has_px = true;
+                }
+                // an id outside the image: the slot asks again in a later batch
+            }
+        }
+    }
+    bool walk = false;
+    int w = -1;
+    f3 rd = mk(0, 0, 0);
+    if (act & has_px) {
+        if (need_ray) {           // camera ray (:514-542)
+            state = pt::seed(lx, y, p.frame_first + k);
+            float ax = 0.0f, ay = 0.0f;
+            if (!(p.flags & PT_FLAG_NO_AA)) {
+                ax = pt::random01(state);
+                ay = pt::random01(state);
+            }
+            const float u = pt::div_mk((float)lx + ax, p.fW, p.rW) - 0.5f;
+            const float v = pt::div_mk((float)y + ay, p.fH, p.rH) - 0.5f;
+            const f3 cfwd = mk(p.cam[3], p.cam[4], p.cam[5]), cright = mk(p.cam[6], p.cam[7], p.cam[8]);
+            const f3 cup = mk(p.cam[9], p.cam[10], p.cam[11]);
+            d = pt::normalize((cfwd + cright * u) + cup * v);
+            o = mk(p.cam[0], p.cam[1], p.cam[2]);
+            inc = mk(0, 0, 0);
+            col = mk(1, 1, 1);
+            bounce = 0;
+            need_ray = false;
+        }
+        // segment set-up: exact-reciprocal guard, spheres (:372-385), walk start
+        const bool fast = (p.scene_fast != 0) & in_guard(o.x, 0x1p-40f, 0x1p60f) & in_guard(o.y, 0x1p-40f, 0x1p60f) &
+                          in_guard(o.z, 0x1p-40f, 0x1p60f) & in_range_abs(d.x, 0x1p-20f, 2.0f) &
+                          in_range_abs(d.y, 0x1p-20f, 2.0f) & in_range_abs(d.z, 0x1p-20f, 2.0f);
+        if (fast) rd = mk(pt::rcp_fast(d.x), pt::rcp_fast(d.y), pt::rcp_fast(d.z));
+        t = __builtin_huge_valf();
+        hprim = -1;
+        if (!(p.flags & PT_FLAG_NO_SPHERES)) {
+            for (int sp = 0; sp < p.sc.n_spheres; sp++) {
+                const float4 c0 = S.spheres[2 * sp];
+                const f3 oc = o - mk(c0.x, c0.y, c0.z);
+                const float a = pt::dot(d, d);
+                const float half_b = pt::dot(oc, d);
+                const float cq = pt::dot(oc, oc) - c0.w;
+                const float disc = half_b * half_b - a * cq;
+                const float ht = disc < 0.0f ? -1.0f : pt::div_g(-half_b - pt::sqrt_g(disc), a);
+                if ((ht > 0.0001f) & (ht < t)) {
+                    t = ht;
+                    hprim = -2 - sp;
+                }
+            }
+        }
+        walk = !(p.flags & PT_FLAG_NO_TRIANGLES) & (p.sc.n_nodes > 0) & !ray_has_nan(o, d);
+        const bool inside = (root_skip >= 0) & fast & (o.x >= p.root_box[0]) & (o.x <= p.root_box[1]) &
+                            (o.y >= p.root_box[2]) & (o.y <= p.root_box[3]) & (o.z >= p.root_box[4]) &
+                            (o.z <= p.root_box[5]);
+        const int img = fast ? oct_base(d, S.np << 5) : 0;
+        w = walk ? (inside ? root_skip : 0) + img : -1;
+        flags = 0u;                // a segment is set up: the next batch finishes it
+    }
+    if (act) {
+        flags |= (need_ray ? kWfNeedRay : 0u) | (has_px ? kWfHasPx : 0u);
+        wf_st(L.r0, s, v4f{o.x, o.y, o.z, t});
+        wf_st(L.r1, s, v4f{d.x, d.y, d.z, __int_as_float(hprim)});
+        wf_st(L.r2, s, v4f{rd.x, rd.y, rd.z, __int_as_float(w)});
+        wf_st(L.q0, s, v4f{col.x, col.y, col.z, __uint_as_float(state)});
+        wf_st(L.q1, s, v4f{inc.x, inc.y, inc.z, __uint_as_float((unsigned)lx | ((unsigned)y << 16))});
+        wf_st(L.q2, s, v4f{__uint_as_float((unsigned)aidx), __uint_as_float((unsigned)k | ((unsigned)kend << 16)),
+                           __uint_as_float((unsigned)bounce | (flags << 8) | (pcost << 16)), __uint_as_float(tile_id)});
+    }
+    // walking segments to the walk queue; a slot still without a pixel (an id outside the
+    // image) or a segment without a walk goes back to the shade queue
+    wf_push(L, kWfQW, act & walk, s);
+    wf_push(L, kWfQS, act & !walk, s);
+    return true;
+}
+
+// NT threads per workgroup; MINW = resident waves per SIMD (the register budget)
+template <bool PADN, int NT, int MINW>
+__global__ __launch_bounds__(NT, MINW) void k_render_wf(KParams p) {
+    resolve_frames(p);
+    extern __shared__ float4 lds[];
+    if ((unsigned)(size_t)(__attribute__((address_space(3))) const char*)g_lds != 0u) __builtin_trap();
+    const int N = PADN ? kPadNodes : p.walk_np, T = p.n_slots, nn = 16 * N, nt = 4 * T;
+    const int nm = 3 * p.n_mats, ns = 2 * p.sc.n_spheres;
+    const int tid = threadIdx.x;
+    for (int i = tid; i < nn; i += NT) lds[i] = p.sc.walk_lds[i];
+    for (int i = tid; i < nt; i += NT) lds[nn + (i & 3) * T + (i >> 2)] = p.sc.tris[i];
+    for (int i = tid; i < nm; i += NT) lds[nn + nt + i] = p.sc.mats[i];
+    for (int i = tid; i < ns; i += NT) lds[nn + nt + nm + i] = p.sc.spheres[i];
+    SceneView S;
+    S.nodes = lds;
+    S.tris = lds + nn;
+    S.mats = lds + nn + nt;
+    S.spheres = lds + nn + nt + nm;
+    S.np = N;
+    S.tp = T;
+    const int P = p.wf_paths;
+    WfLds L;
+    L.r0 = nn + nt + nm + ns;
+    L.r1 = L.r0 + P;
+    L.r2 = L.r1 + P;
+    L.q0 = L.r2 + P;
+    L.q1 = L.q0 + P;
+    L.q2 = L.q1 + P;
+    L.ring = (unsigned)(L.q2 + P) << 4;
+    L.rmask = (unsigned)p.wf_ring - 1u;
+    L.ctr = L.ring + 3u * (unsigned)p.wf_ring * 2u;
+    // every slot starts fresh (no pixel) in the shade queue, which hands it its first item
+    for (int i = tid; i < 3 * p.wf_ring / 2; i += NT) *(lds_u32*)(size_t)(L.ring + 4u * i) = 0u;
+    if (tid < 16) *wf_ctr(L, tid) = 0u;
+    __syncthreads();
+    for (int sl = tid; sl < P; sl += NT) {
+        wf_st(L.q2, sl, v4f{0.0f, 0.0f, __uint_as_float((kWfFresh | kWfNeedRay) << 8), __uint_as_float(~0u)});
+        *(lds_u16*)(size_t)(L.ring + 2u * ((unsigned)kWfQS * (unsigned)p.wf_ring + sl)) = (unsigned short)(sl + 1);
+    }
+    if (tid == 0) {
+        *wf_ctr(L, 3 * kWfQS) = (unsigned)P;
+        *wf_ctr(L, 3 * kWfQS + 2) = (unsigned)P;
+        *wf_ctr(L, kWfLive) = (unsigned)P;
+    }
+    __syncthreads();
+
+    const int tiles_x = (p.W + 7) >> 3;
+    const unsigned n_groups = (unsigned)((p.n_frames + p.group - 1) / p.group);
+    const unsigned total_ids = (unsigned)tiles_x * (unsigned)((p.rows_local + 7) >> 3) * n_groups * 64u;
+    const int root_skip = p.root_child < 0 ? -1 : p.root_child << 4;
+
+    // the wave's walkers (w < 0: lane free, slot -1 once its ray is queued)
+    int slot = -1, w = -1;
+    f3 o = mk(0, 0, 0), d = mk(0, 0, 1), rd = mk(0, 0, 0);
+    float t = 0.0f;
+    bool fast = false;
+    unsigned long long idle_t0 = 0;       // watchdog: start of the current idle stretch
+    WfDiag dg;
+#ifdef PT_WF_DIAG
+    unsigned long long dclk = clock64();
+#define WF_CLK(i) do { const unsigned long long c1_ = clock64(); WF_DIAG(i, c1_ - dclk); dclk = c1_; } while (0)
+#else
+#define WF_CLK(i) do { } while (0)
+#endif
+    for (;;) {
+        const unsigned aL = wf_peek(L, 3 * kWfQL + 2), aS = wf_peek(L, 3 * kWfQS + 2);
+        // full batches (all 64 lanes, or none when another wave took them first)
+        if ((int)aL >= p.wf_leaf_min && wf_leaf_batch(p, S, L, dg, p.wf_leaf_min >= 64)) { idle_t0 = 0; WF_CLK(8); continue; }
+        if ((int)aS >= p.wf_shade_min &&
+            wf_shade_batch(p, S, L, total_ids, n_groups, root_skip, dg, p.wf_shade_min >= 64)) {
+            idle_t0 = 0;
+            WF_CLK(9);
+            continue;
+        }
+        // refill free lanes from the walk queue
+        const unsigned long long freem = __ballot(w < 0);
+        if (freem) {
+            const int s = wf_pop(L, kWfQW, freem, p.wf_err, dg);
+            if (s >= 0) {
+                const v4f a0 = wf_ld(L.r0, s), a1 = wf_ld(L.r1, s), a2 = wf_ld(L.r2, s);
+                o = mk(a0.x, a0.y, a0.z);
+                t = a0.w;
+                d = mk(a1.x, a1.y, a1.z);
+                rd = mk(a2.x, a2.y, a2.z);
+                w = __float_as_int(a2.w);
+                fast = a2.x != 0.0f;
+                slot = s;
+            }
+            WF_DIAG(11, __popcll(__ballot(s >= 0)));
+        }
+        if (__any(w >= 0)) {
+            idle_t0 = 0;
+            if (__all(fast || w < 0)) wf_walk<true, PADN>(S, o, d, rd, fast, t, p.wf_refill, w, dg);
+            else wf_walk<false, PADN>(S, o, d, rd, fast, t, p.wf_refill, w, dg);
+            // stopped rays: at a hit leaf (w <= -2) to the leaf queue, walk ended (-1) to shading
+            const bool stopped = (w < 0) & (slot >= 0);
+            if (stopped & (w <= -2)) wf_stw(L.r2, slot, __int_as_float(w));
+            wf_push(L, kWfQL, stopped & (w <= -2), slot);
+            wf_push(L, kWfQS, stopped & (w == -1), slot);
+            if (stopped) slot = -1;
+            WF_CLK(7);
+            continue;
+        }
+        // nothing to walk: drain whatever the queues hold, else wait for the other waves
+        if (aL && wf_leaf_batch(p, S, L, dg, false)) { idle_t0 = 0; WF_CLK(8); continue; }
+        if (aS && wf_shade_batch(p, S, L, total_ids, n_groups, root_skip, dg, false)) { idle_t0 = 0; WF_CLK(9); continue; }
+        if (wf_peek(L, kWfLive) == 0u) break;
+        // watchdog (100 MHz clock): idle for 2 s while paths are live means a lost path;
+        // give up (the host reports PT_E_HIP) rather than spin forever
+        const unsigned long long now = __builtin_amdgcn_s_memrealtime();
+        if (idle_t0 == 0) idle_t0 = now;
+        else if (now - idle_t0 > 200000000ull) {
+            if (lane_id() == 0) atomicAdd(p.wf_err, 1u);
+            break;
+        }
+        __builtin_amdgcn_s_sleep(2);
+        WF_DIAG(6, 1);
+        WF_CLK(10);
+    }
+#undef WF_CLK
+    dg.flush();
+}
+
 // ACES film tonemap epilogue (screenQuadFrag.c:12-26) -> RGBA8, alpha 255.
 __global__ __launch_bounds__(256) void k_aces(const float4* __restrict__ src, uchar4* __restrict__ dst,
                                               long long n) {
@@ -1532,6 +2107,9 @@ struct pt_ctx {
     int leaf_thresh = 0, shade_thresh = 0, minw = 0, trav_floor = 0, compact_max = 63;
     // frame-split work items (KParams::group): 0 = automatic, n = frames per item
     int group_force = 0;
+    // variant 4 knobs (0 = automatic): path slots per workgroup, refill walker count,
+    // leaf / shade batch minimum
+    int wf_paths = 0, wf_refill = 0, wf_leaf_min = 0, wf_shade_min = 0, wf_threads = 0;
     int n_cu = 0;
     float* d_rgb = nullptr;        // per-(frame, pixel) colours of the frame-split mode
     size_t rgb_bytes = 0;
@@ -1548,6 +2126,7 @@ struct pt_ctx {
     float last_ms = 0.0f;
     unsigned long long last_counts[16] = {0};
     bool count_pending = false;
+    bool wf_check = false;          // a variant-4 launch is pending: check its watchdog word
     std::string err;
 };
 
@@ -1894,8 +2473,9 @@ int pt_set_counting(pt_ctx* c, int enable) {
 
 int pt_set_kernel(pt_ctx* c, int variant) {
     if (!c) return PT_E_ARG;
-    if (variant < 0 || variant > 3)
-        return fail(c, PT_E_ARG, "unknown kernel variant (0 state machine, 1 tiled, 2 while-while, 3 state machine / global scene)");
+    if (variant < 0 || variant > 4)
+        return fail(c, PT_E_ARG, "unknown kernel variant (0 state machine, 1 tiled, 2 while-while, 3 state machine / "
+                                 "global scene, 4 wavefront queues)");
     c->variant = variant;
     drop_graph(c);
     return PT_OK;
@@ -1912,6 +2492,20 @@ int pt_set_tuning(pt_ctx* c, int key, int value) {
         } else {
             c->scratch_budget = (size_t)value << 20;
         }
+        drop_graph(c);
+        return PT_OK;
+    }
+    if (key == 14) {
+        if (value != 0 && value != 512 && value != 768 && value != 896 && value != 1024)
+            return fail(c, PT_E_ARG, "wavefront workgroup size must be 512, 768, 896 or 1024 (0 = automatic)");
+        c->wf_threads = value;
+        drop_graph(c);
+        return PT_OK;
+    }
+    if (key >= 10 && key <= 13) {
+        if (value < 0 || (key == 10 && value > 1536) || (key > 10 && value > 64))
+            return fail(c, PT_E_ARG, "wavefront knob out of range");
+        (key == 10 ? c->wf_paths : key == 11 ? c->wf_refill : key == 12 ? c->wf_leaf_min : c->wf_shade_min) = value;
         drop_graph(c);
         return PT_OK;
     }
@@ -1962,7 +2556,7 @@ int pt_set_tuning(pt_ctx* c, int key, int value) {
 // items a 1080p/8 share of a 1024-frame launch would run each lane through 1024 frames
 // in sequence (minutes).
 static int plan_group(const pt_ctx* c, int n_frames) {
-    if (c->variant != 0 && c->variant != 3) return n_frames;
+    if (c->variant != 0 && c->variant != 3 && c->variant != 4) return n_frames;
     if (c->group_force > 0) return std::min(c->group_force, n_frames);
     const int waves = c->minw ? c->minw : 6;
     const double lanes = (double)c->n_cu * 4.0 * waves * 64.0;
@@ -1989,6 +2583,24 @@ static int ensure_rgb(pt_ctx* c, int n_frames) {
     return PT_OK;
 }
 
+// Variant 4 (wavefront queues) runs when the scene is staged in LDS with room beside it for
+// the path slots (96 B each), raysPerPixel is 1, nothing is counted and the packed path
+// counters fit (bounce < 256, frames per launch < 2^16); it always stores per-frame colours.
+// Otherwise variant 4 falls back to the state-machine kernel (variant 0).  Returns the path
+// slots per workgroup, 0 when variant 4 does not run.
+static int wf_threads(const pt_ctx* c) { return c->wf_threads ? c->wf_threads : 1024; }
+static int wf_paths(const pt_ctx* c, int n_frames) {
+    if (c->variant != 4 || c->counting || c->cfg.rays_per_pixel != 1 || c->cfg.max_bounce > 250 || n_frames > 65535)
+        return 0;
+    if (c->lds_bytes > kLdsSceneMax) return 0;
+    const int per_cu = wf_threads(c) <= 512 ? 4 : (wf_threads(c) < 1024 ? 2 : 1);   // workgroups per CU
+    // 96 B of records per path slot plus 3 ring entries (2 B, rings of at most 2x the slots)
+    const long long room = 160 * 1024 / per_cu - (long long)c->lds_bytes - 64;
+    const int fit = (int)std::min<long long>(room / (96 + 12), 1536);
+    const int P = c->wf_paths ? std::min(c->wf_paths, fit) : fit;
+    return P >= 64 ? P : 0;
+}
+
 // Queue ids are 32-bit: a launch's items * 64 plus what the resident waves can reserve past
 // the end (each wave pulls at most 64 ids, twice after the queue ran dry) stay below 2^32.
 constexpr unsigned long long kIdLimit = (1ull << 32) - (1ull << 24);
@@ -2003,7 +2615,7 @@ static int launch_frames(const pt_ctx* c, int n_frames) {
     int n = n_frames;
     for (;;) {
         const int g = plan_group(c, n);
-        if (g >= n) return n;                       // register mode: no scratch, one group
+        if (g >= n && !wf_paths(c, n)) return n;    // register mode: no scratch, one group
         const unsigned long long by_budget = c->scratch_budget / (px * 12ull);
         const unsigned long long ng = (unsigned long long)((n + g - 1) / g);
         const unsigned long long by_ids = (kIdLimit / tiles64) * (unsigned long long)g;
@@ -2071,7 +2683,8 @@ static int enqueue_render(pt_ctx* c, int frame_first, int n_frames, int acc_firs
         const unsigned long long items = (unsigned long long)c->n_tiles * ng;
         p.grp_magic = (ng > 1 && items * ng < (1ull << 32)) ? (unsigned)(((1ull << 32) + ng - 1) / ng) : 0u;
     }
-    if (p.group < n_frames) {
+    const int wfP = wf_paths(c, n_frames);
+    if (p.group < n_frames || wfP) {
         int rc = ensure_rgb(c, n_frames);
         if (rc) return rc;
         p.rgb = c->d_rgb;
@@ -2082,9 +2695,39 @@ static int enqueue_render(pt_ctx* c, int frame_first, int n_frames, int acc_firs
     if (c->rows_local == 0) return PT_OK;
     // variants: 0 state-machine persistent (default), 1 one-lane-per-pixel tiles,
     // 2 while-while persistent, 3 = 0 with the scene forced to stay in global memory
-    bool use_lds = (c->variant == 0 || c->variant == 2) && c->lds_bytes <= kLdsSceneMax;
-    if (c->variant != 1) HIPCHK(c, hipMemsetAsync(c->d_work, 0, sizeof(unsigned), c->stream));
-    if (c->variant == 1) {
+    const int variant = c->variant == 4 ? 0 : c->variant;   // variant 4's fallback is variant 0
+    bool use_lds = (variant == 0 || variant == 2) && c->lds_bytes <= kLdsSceneMax;
+    if (variant != 1 && !wfP) HIPCHK(c, hipMemsetAsync(c->d_work, 0, sizeof(unsigned), c->stream));
+    if (wfP) {
+        HIPCHK(c, hipMemsetAsync(c->d_work, 0, 8 * sizeof(unsigned), c->stream));
+        c->wf_check = true;
+        // one 1024-thread workgroup per CU (16 waves share the scene copy and wfP path
+        // slots); no more workgroups than the pixel-frame items fill
+        p.wf_paths = wfP;
+        p.wf_ring = 64;
+        while (p.wf_ring < wfP) p.wf_ring <<= 1;
+        p.wf_err = c->d_work + 4;            // reset with the queue counter below
+        p.wf_refill = c->wf_refill ? c->wf_refill : 16;     // keysweep: 16 +4% over 40
+        p.wf_leaf_min = c->wf_leaf_min ? c->wf_leaf_min : 64;
+        p.wf_shade_min = c->wf_shade_min ? c->wf_shade_min : 64;
+        const size_t lds = c->lds_bytes + 96 * (size_t)wfP + 3 * (size_t)p.wf_ring * 2 + 64;
+        const unsigned long long ids = (unsigned long long)c->n_tiles * 64ull *
+                                       (unsigned long long)((n_frames + p.group - 1) / p.group);
+        const int nt = wf_threads(c);
+        const unsigned per_cu = nt <= 512 ? 4u : (nt < 1024 ? 2u : 1u);
+        const unsigned grid = (unsigned)std::min<unsigned long long>(
+            (unsigned long long)c->n_cu * per_cu, std::max(1ull, (ids + wfP - 1) / (unsigned long long)wfP));
+#define PT_WF(NT)                                                                                             \
+    if (c->walk_np == kPadNodes) hipLaunchKernelGGL((k_render_wf<true, NT, NT / 64 * (NT <= 512 ? 4 : (NT < 1024 ? 2 : 1)) / 4>), dim3(grid), dim3(NT), lds, c->stream, p); \
+    else hipLaunchKernelGGL((k_render_wf<false, NT, NT / 64 * (NT <= 512 ? 4 : (NT < 1024 ? 2 : 1)) / 4>), dim3(grid), dim3(NT), lds, c->stream, p);
+        if (nt == 512) { PT_WF(512) }
+        else if (nt == 768) { PT_WF(768) }
+        else if (nt == 896) { PT_WF(896) }
+        else { PT_WF(1024) }
+#undef PT_WF
+        long long px = (long long)c->rows_local * p.W;
+        hipLaunchKernelGGL(k_accum_frames, dim3((unsigned)((px + 255) / 256)), dim3(256), 0, c->stream, p);
+    } else if (variant == 1) {
         dim3 grid((p.W + 15) / 16, (c->rows_local + 15) / 16);
         if (c->counting)
             hipLaunchKernelGGL(k_render_tiled<true>, grid, dim3(256), 0, c->stream, p);
@@ -2119,7 +2762,7 @@ static int enqueue_render(pt_ctx* c, int frame_first, int n_frames, int acc_firs
     else if (p.rgb) hipLaunchKernelGGL((k_render_sm<false, L, 5, M, true>), grid, dim3(256), L ? lds : top_lds, c->stream, p); \
     else if (mw >= 6) hipLaunchKernelGGL((k_render_sm<false, L, 6, M, false>), grid, dim3(256), L ? lds : top_lds, c->stream, p); \
     else hipLaunchKernelGGL((k_render_sm<false, L, 5, M, false>), grid, dim3(256), L ? lds : top_lds, c->stream, p);
-        if (c->variant == 0 || c->variant == 3) {
+        if (variant == 0 || variant == 3) {
             bool multi = p.rpp > 1;
             if (use_lds && multi) { PT_LAUNCH_SM(true, true) }
             else if (use_lds) { PT_LAUNCH_SM(true, false) }
@@ -2261,7 +2904,8 @@ int pt_progressive_run(pt_ctx* c, int replays) {
     c->ev_pending.emplace_back(ev[0], ev[1]);
     HIPCHK(c, hipEventRecord(ev[0], c->stream));
     for (int r = 0; r < replays; r++) HIPCHK(c, hipGraphLaunch(c->graph_exec, c->stream));
-    if (c->adaptive && (c->variant == 0 || c->variant == 3)) c->cost_pending = true;
+    if (c->adaptive && (c->variant == 0 || c->variant == 3 || c->variant == 4)) c->cost_pending = true;
+    if (c->variant == 4) c->wf_check = true;
     HIPCHK(c, hipEventRecord(ev[1], c->stream));
     return PT_OK;
 }
@@ -2280,6 +2924,12 @@ int pt_sync(pt_ctx* c) {
         c->ev_free.push_back(pr.second);
     }
     c->ev_pending.clear();
+    if (c->wf_check) {
+        unsigned trips = 0;
+        HIPCHK(c, hipMemcpy(&trips, c->d_work + 4, sizeof(unsigned), hipMemcpyDeviceToHost));
+        c->wf_check = false;
+        if (trips) return fail(c, PT_E_HIP, "wavefront kernel watchdog tripped (" + std::to_string(trips) + " waves)");
+    }
     if (c->count_pending) {
         HIPCHK(c, hipMemcpy(c->last_counts, c->d_counters, 16 * sizeof(unsigned long long), hipMemcpyDeviceToHost));
         c->count_pending = false;
@@ -2388,6 +3038,18 @@ extern "C" int pt_debug_phase_clock(unsigned long long out[8], int reset) {
     if (reset) {
         unsigned long long z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
         if (hipMemcpyToSymbol(HIP_SYMBOL(g_phase_clk), z, sizeof(z)) != hipSuccess) return -1;
+    }
+    return 0;
+}
+#endif
+
+#ifdef PT_WF_DIAG
+extern "C" int pt_debug_wf_diag(unsigned long long out[16], int reset) {
+    if (hipDeviceSynchronize() != hipSuccess) return -1;
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_wf_diag), sizeof(unsigned long long) * 16) != hipSuccess) return -1;
+    if (reset) {
+        unsigned long long z[16] = {0};
+        if (hipMemcpyToSymbol(HIP_SYMBOL(g_wf_diag), z, sizeof(z)) != hipSuccess) return -1;
     }
     return 0;
 }

@@ -298,6 +298,10 @@ class PathTracer:
         if scratch_mib is not None:
             self._check(lib().pt_set_tuning(self.h, 8, int(scratch_mib)))
 
+    def set_key(self, key, value):
+        """Raw pt_set_tuning(key, value) (experiments)."""
+        self._check(lib().pt_set_tuning(self.h, int(key), int(value)))
+
     def dispatch(self, frame, accumulate):
         """One glDispatchCompute with uniforms frame/accumulate (ogl_path_trace.h:176-183)."""
         self._check(lib().pt_render(self.h, frame, 1, accumulate))

@@ -1,5 +1,3 @@
-cd "$GRAFT_REPO_ROOT"; mkdir -p gpurun_out
-timeout -k 10 600 python tools/ab_inproc.py --libs cur,u2,u6,u8 --rounds 3 --scene bunny --spp 64 --chunk 64 > gpurun_out/ab_c3.log 2>&1 || exit $?
-echo "C3:"; grep median gpurun_out/ab_c3.log
-timeout -k 10 600 python tools/ab_inproc.py --libs cur,u2,u6,u8 --rounds 3 --scene sponza --spp 32 --chunk 32 > gpurun_out/ab_c4.log 2>&1 || exit $?
-echo "C4:"; grep median gpurun_out/ab_c4.log
+cd $GRAFT_REPO_ROOT; mkdir -p gpurun_out
+timeout -k 10 300 python -u tools/keysweep.py --variant 4 --spp 64 --configs "11=40;11=16;11=24;11=32;11=52;12=48,13=48;10=1024" --rounds 2 > gpurun_out/ks_a.log 2>&1 || exit $?
+grep median gpurun_out/ks_a.log
