@@ -15,6 +15,7 @@ ap = argparse.ArgumentParser()
 ap.add_argument("--spp", type=int, default=64)
 ap.add_argument("--scene", default="cornell")
 ap.add_argument("--keys", default="")
+ap.add_argument("--variant", type=int, default=4)
 a = ap.parse_args()
 sb = pt_host.setupBuffers(*pt_scenes.write_scene(a.scene, os.path.join(REPO, "scenes")))
 pt = pt_host.PathTracer(1920, 1080, max_bounce=8)
@@ -23,7 +24,7 @@ pt.set_counting(True)
 pt.render(1, a.spp, 0)
 seg = pt.stats()[1]["segments"]
 pt.set_counting(False)
-pt.set_kernel(4)
+pt.set_kernel(a.variant)
 for kv in filter(None, a.keys.split(",")):
     k, v = kv.split("=")
     pt.set_key(int(k), int(v))
