@@ -12,9 +12,12 @@
 //                slab axis is one packed-f32 register pair)
 //                internal: a = hit link (left child), b = miss
 //                leaf:     a = ~(slot<<1 | single), b = next
-//   tri   64 B : {v0.xyz, n.x}, {v1.xyz, n.y}, {v2.xyz, n.z}, {d0, matIdx, 0, 0}
+//   tri   64 B : {n.xyz, d0}, {v0.xyz, cont}, {v1.xyz, matIdx}, {v2.xyz, 0}
 //                n = normalize(cross(v1-v0, v2-v0)) and d0 = -dot(n, v0) are the exact values
-//                hit_triangle recomputes per call; a leaf's triangles sit in slots 2k, 2k+1.
+//                hit_triangle recomputes per call; a leaf's triangles sit in slots 2k, 2k+1;
+//                the plane test reads one quad, shading two (quads 0 and 2).  cont: the LDS
+//                walk's continuation of the leaf (first slot only).
+//   leaf code  : k << 2 | coplanar << 1 | single (k = leaf pair index, slots 2k and 2k+1)
 //   mat   48 B : {color.rgb, smoothness}, {emission*strength, specProb}, {specular.rgb, 0}
 //   sphere 32 B: {c.xyz, r*r}, {matIdx, 0, 0, 0}
 #include "pt_math.h"
@@ -145,11 +148,11 @@ __device__ __forceinline__ bool slab(float4 A, float4 B, f3 o, f3 d, float cur_t
 // value behaves like a miss in that choice, so culling before the edge tests is exact.
 __device__ __forceinline__ float tri_hit(const float4* T, f3 o, f3 d, float tbest, f3& n) {
     float4 q0 = T[0], q1 = T[1], q2 = T[2], q3 = T[3];
-    n = mk(q0.w, q1.w, q2.w);
-    float t = -(pt::dot(n, o) + q3.x) / pt::dot(n, d);
+    n = mk(q0.x, q0.y, q0.z);
+    float t = -(pt::dot(n, o) + q0.w) / pt::dot(n, d);
     if (t < 0.0f) return -1.0f;
     if (!(t < tbest)) return -1.0f;
-    f3 v0 = mk(q0.x, q0.y, q0.z), v1 = mk(q1.x, q1.y, q1.z), v2 = mk(q2.x, q2.y, q2.z);
+    f3 v0 = mk(q1.x, q1.y, q1.z), v1 = mk(q2.x, q2.y, q2.z), v2 = mk(q3.x, q3.y, q3.z);
     f3 p = o + d * t;
     if (!(pt::dot(n, pt::cross(v1 - v0, p - v0)) > 0.0f)) return -1.0f;
     if (!(pt::dot(n, pt::cross(v2 - v1, p - v1)) > 0.0f)) return -1.0f;
@@ -192,8 +195,8 @@ __device__ __forceinline__ float tri_mt(float4 q0, float4 q1, float4 q2, f3 o, f
 }
 __device__ __forceinline__ float tri_test(int flags, const float4* T, f3 o, f3 d, float tbest, f3& n) {
     if (flags & PT_FLAG_MOLLER_TRUMBORE) {
-        n = mk(T[0].w, T[1].w, T[2].w);
-        return tri_mt(T[0], T[1], T[2], o, d);
+        n = mk(T[0].x, T[0].y, T[0].z);
+        return tri_mt(T[1], T[2], T[3], o, d);
     }
     return tri_hit(T, o, d, tbest, n);
 }
@@ -238,7 +241,7 @@ __device__ __forceinline__ bool collide(const KParams& p, f3 o, f3 d, f3& normal
         if (hb && a < 0) {
             if (COUNT) c.tri += 2;
             int code = ~a;
-            const float4* T0 = p.sc.tris + 8 * (code >> 1);
+            const float4* T0 = p.sc.tris + 8 * (code >> 2);
             f3 n0, n1;
             float h1 = tri_test(p.flags, T0, o, d, t, n0);
             float h2 = (code & 1) ? h1 : tri_test(p.flags, T0 + 4, o, d, t, n1);
@@ -249,14 +252,14 @@ __device__ __forceinline__ bool collide(const KParams& p, f3 o, f3 d, f3& normal
                 t = h1;
                 normal = n0;
                 hitp = o + d * h1;
-                mat = __float_as_int(T0[3].y);
+                mat = __float_as_int(T0[2].w);
             } else if (h2 > 0.0001f && h2 < t) {
                 if (pt::dot(n1, d) > 0.0f) n1 = n1 * -1.0f;
                 hit = true;
                 t = h2;
                 normal = n1;
                 hitp = o + d * h2;
-                mat = __float_as_int(T0[(code & 1) ? 3 : 7].y);
+                mat = __float_as_int(T0[(code & 1) ? 2 : 6].w);
             }
         }
         bi = next;
@@ -423,9 +426,10 @@ struct SceneView {
 // box hit and after a miss, as byte offsets of the node (16 * index, its lo-plane entry) or
 // -1 (chain ends):
 //   internal node: (first child, next-right)
-//   leaf node:     (-2 - code, next-right), code = slot << 1 | single: a hit stops the walk
+//   leaf node:     (-2 - code, next-right), code = k << 2 | coplanar << 1 | single: a hit
+//                  stops the walk
 // so one select is the whole link step.  The leaf's continuation (its next-right) rides in
-// the spare .z of its first triangle's 4th quad, which the leaf test loads anyway.
+// the spare .w of its first triangle's quad 1 (beside v0).
 // The LDS walk holds 8 such images, one per octant of ray directions (image k at byte
 // 32 * N * k, links absolute inside their image): image k stores the bounds of each axis
 // whose direction sign bit is set in k swapped, near bound first (slab_oct); image 0 is the
@@ -562,7 +566,7 @@ __device__ __forceinline__ bool collide_v(const SceneView& S, int n_nodes, int n
         if (hb && a < 0) {
             if (COUNT) c.tri += 2;
             int code = ~a;
-            const float4* T0 = S.tris + 8 * (code >> 1);
+            const float4* T0 = S.tris + 8 * (code >> 2);
             f3 n0, n1;
             float h1 = tri_test(flags, T0, o, d, t, n0);
             float h2 = h1;
@@ -574,14 +578,14 @@ __device__ __forceinline__ bool collide_v(const SceneView& S, int n_nodes, int n
                 t = h1;
                 normal = n0;
                 hitp = o + d * h1;
-                mat = __float_as_int(T0[3].y);
+                mat = __float_as_int(T0[2].w);
             } else if (h2 > 0.0001f && h2 < t) {
                 if (pt::dot(n1, d) > 0.0f) n1 = n1 * -1.0f;
                 hit = true;
                 t = h2;
                 normal = n1;
                 hitp = o + d * h2;
-                mat = __float_as_int(T0[(code & 1) ? 3 : 7].y);
+                mat = __float_as_int(T0[(code & 1) ? 2 : 6].w);
             }
         }
         bi = next;
@@ -594,9 +598,9 @@ __device__ __forceinline__ bool collide_v(const SceneView& S, int n_nodes, int n
 // Same operations, same bits as tri_hit().
 __device__ __forceinline__ float tri_hit_bf(const float4* T, f3 o, f3 d, float tbest, f3& n) {
     float4 q0 = T[0], q1 = T[1], q2 = T[2], q3 = T[3];
-    n = mk(q0.w, q1.w, q2.w);
-    float t = -(pt::dot(n, o) + q3.x) / pt::dot(n, d);
-    f3 v0 = mk(q0.x, q0.y, q0.z), v1 = mk(q1.x, q1.y, q1.z), v2 = mk(q2.x, q2.y, q2.z);
+    n = mk(q0.x, q0.y, q0.z);
+    float t = -(pt::dot(n, o) + q0.w) / pt::dot(n, d);
+    f3 v0 = mk(q1.x, q1.y, q1.z), v1 = mk(q2.x, q2.y, q2.z), v2 = mk(q3.x, q3.y, q3.z);
     f3 p = o + d * t;
     float e0 = pt::dot(n, pt::cross(v1 - v0, p - v0));
     float e1 = pt::dot(n, pt::cross(v2 - v1, p - v1));
@@ -609,15 +613,14 @@ __device__ __forceinline__ float tri_hit_bf(const float4* T, f3 o, f3 d, float t
 // lane of the wave still needs them (a wave-uniform skip; per lane the verdict is the
 // same select as tri_hit_bf, so the bits are identical).
 template <bool LDS>
-__device__ __forceinline__ float tri_hit_lazy(const SceneView& S, int slot, float4 q3, f3 o, f3 d, float tbest,
+__device__ __forceinline__ float tri_hit_lazy(const SceneView& S, int slot, float4 nd, f3 o, f3 d, float tbest,
                                               f3& n) {
-    float4 q0 = tri_quad<LDS>(S, slot, 0), q1 = tri_quad<LDS>(S, slot, 1);
-    float4 q2 = tri_quad<LDS>(S, slot, 2);      // q3: loaded by the caller
-    n = mk(q0.w, q1.w, q2.w);
-    float t = -(pt::dot(n, o) + q3.x) / pt::dot(n, d);
+    n = mk(nd.x, nd.y, nd.z);    // nd: quad 0 {n, d0}, loaded by the caller
+    float t = -(pt::dot(n, o) + nd.w) / pt::dot(n, d);
     bool ok = !(t < 0.0f) && (t < tbest);
     if (__any(ok)) {
-        f3 v0 = mk(q0.x, q0.y, q0.z), v1 = mk(q1.x, q1.y, q1.z), v2 = mk(q2.x, q2.y, q2.z);
+        const float4 q1 = tri_quad<LDS>(S, slot, 1), q2 = tri_quad<LDS>(S, slot, 2), q3 = tri_quad<LDS>(S, slot, 3);
+        f3 v0 = mk(q1.x, q1.y, q1.z), v1 = mk(q2.x, q2.y, q2.z), v2 = mk(q3.x, q3.y, q3.z);
         f3 p = o + d * t;
         float e0 = pt::dot(n, pt::cross(v1 - v0, p - v0));
         float e1 = pt::dot(n, pt::cross(v2 - v1, p - v1));
@@ -631,26 +634,16 @@ __device__ __forceinline__ float tri_hit_lazy(const SceneView& S, int slot, floa
 // (:285-297) and the three edge tests at that distance (:299-306), the same operations as
 // tri_hit_bf in the same order, so the same bits.
 template <bool LDS>
-__device__ __forceinline__ float tri_plane(const SceneView& S, int slot, float4 q3, f3 o, f3 d) {
-    const f3 n = mk(tri_quad<LDS>(S, slot, 0).w, tri_quad<LDS>(S, slot, 1).w, tri_quad<LDS>(S, slot, 2).w);
-    return -(pt::dot(n, o) + q3.x) / pt::dot(n, d);
+__device__ __forceinline__ float tri_plane(float4 nd, f3 o, f3 d) {    // nd: quad 0 {n, d0}
+    const f3 n = mk(nd.x, nd.y, nd.z);
+    return -(pt::dot(n, o) + nd.w) / pt::dot(n, d);
 }
+// The three edge tests (:299-306) of triangle `slot` at p with normal n: the caller has n
+// from the plane test (quad 0), so only the vertices (quads 1-3) are read.
 template <bool LDS>
-__device__ __forceinline__ bool tri_edges(const SceneView& S, int slot, f3 o, f3 d, float t) {
-    const float4 q0 = tri_quad<LDS>(S, slot, 0), q1 = tri_quad<LDS>(S, slot, 1), q2 = tri_quad<LDS>(S, slot, 2);
-    const f3 n = mk(q0.w, q1.w, q2.w);
-    const f3 v0 = mk(q0.x, q0.y, q0.z), v1 = mk(q1.x, q1.y, q1.z), v2 = mk(q2.x, q2.y, q2.z);
-    const f3 p = o + d * t;
-    const float e0 = pt::dot(n, pt::cross(v1 - v0, p - v0));
-    const float e1 = pt::dot(n, pt::cross(v2 - v1, p - v1));
-    const float e2 = pt::dot(n, pt::cross(v0 - v2, p - v2));
-    return (e0 > 0.0f) & (e1 > 0.0f) & (e2 > 0.0f);
-}
-template <bool LDS>
-__device__ __forceinline__ bool tri_edges_at(const SceneView& S, int slot, f3 p) {
-    const float4 q0 = tri_quad<LDS>(S, slot, 0), q1 = tri_quad<LDS>(S, slot, 1), q2 = tri_quad<LDS>(S, slot, 2);
-    const f3 n = mk(q0.w, q1.w, q2.w);
-    const f3 v0 = mk(q0.x, q0.y, q0.z), v1 = mk(q1.x, q1.y, q1.z), v2 = mk(q2.x, q2.y, q2.z);
+__device__ __forceinline__ bool tri_edges_at(const SceneView& S, int slot, f3 n, f3 p) {
+    const float4 q1 = tri_quad<LDS>(S, slot, 1), q2 = tri_quad<LDS>(S, slot, 2), q3 = tri_quad<LDS>(S, slot, 3);
+    const f3 v0 = mk(q1.x, q1.y, q1.z), v1 = mk(q2.x, q2.y, q2.z), v2 = mk(q3.x, q3.y, q3.z);
     const float e0 = pt::dot(n, pt::cross(v1 - v0, p - v0));
     const float e1 = pt::dot(n, pt::cross(v2 - v1, p - v1));
     const float e2 = pt::dot(n, pt::cross(v0 - v2, p - v2));
@@ -685,19 +678,25 @@ __device__ __forceinline__ float fperm_f(int dst_bytes, float v) {
 // pass of edge tests serves both triangles of every lane; a ballot returns the verdicts.  More than 63 pairs: each lane tests its own.  Every edge
 // test runs the same operations on the same values as at its source lane: the same bits.
 // Returns (through h1 / h2) the hit_triangle results up to that equivalence.
+// nda: quad 0 {n, d0} of slot s0; cop: the leaf code's coplanar bit.
 template <bool LDS>
-__device__ __forceinline__ void leaf_pair_tests(const SceneView& S, bool at, int s0, float4 q3a,
+__device__ __forceinline__ void leaf_pair_tests(const SceneView& S, bool at, int s0, float4 nda, bool cop,
                                                 f3 o, f3 d, float t, int max_pairs, float& h1, float& h2) {
     float ta = 0.0f, tb = 0.0f;
-    if (at) ta = tri_plane<LDS>(S, s0, q3a, o, d);
-    // a coplanar pair (q3a.w != 0: n and d0 equal up to the sign of zero components, flagged
-    // at upload) has the same plane distance wherever it can pass the acceptance tests, so
-    // the second one is only computed when some lane's leaf is not such a pair
-    const bool cop = q3a.w != 0.0f;
+    if (at) ta = tri_plane<LDS>(nda, o, d);
+    // a coplanar pair (n and d0 equal up to the sign of zero components, flagged at upload)
+    // has the same plane distance wherever it can pass the acceptance tests, so the second
+    // one is only computed when some lane's leaf is not such a pair.  Its edge tests may use
+    // the first triangle's n: a zero factor of either sign cannot change a `> 0` verdict.
+    float4 ndb = nda;
     if (__any(at & !cop)) {
-        if (at & !cop) tb = tri_plane<LDS>(S, s0 + 1, tri_quad<LDS>(S, s0 + 1, 3), o, d);
+        if (at & !cop) {
+            ndb = tri_quad<LDS>(S, s0 + 1, 0);
+            tb = tri_plane<LDS>(ndb, o, d);
+        }
     }
     tb = cop ? ta : tb;
+    const f3 na3 = mk(nda.x, nda.y, nda.z), nb3 = mk(ndb.x, ndb.y, ndb.z);
     const bool na = at & (ta > 0.0001f) & (ta < t);
     const bool nb = at & (tb >= 0.0001f) & (tb < t);
     const unsigned long long ma = __ballot(na), mb = __ballot(nb);
@@ -718,14 +717,25 @@ __device__ __forceinline__ void leaf_pair_tests(const SceneView& S, bool at, int
         const int as = __builtin_amdgcn_ds_permute(da, s0), bs = __builtin_amdgcn_ds_permute(db, s0 + 1);
         const f3 wp = first ? mk(ax, ay, az) : mk(bx, by, bz);
         const int ws = first ? as : bs;
+        // the worker's normal: re-read from LDS, or for a global-memory scene (where the
+        // loads, not the permutes, set the pace) handed over with the hit point
+        f3 wn;
+        if (LDS) {
+            const float4 q0 = tri_quad<LDS>(S, ws, 0);
+            wn = mk(q0.x, q0.y, q0.z);
+        } else {
+            const float nax = fperm_f(da, na3.x), nay = fperm_f(da, na3.y), naz = fperm_f(da, na3.z);
+            const float nbx = fperm_f(db, nb3.x), nby = fperm_f(db, nb3.y), nbz = fperm_f(db, nb3.z);
+            wn = first ? mk(nax, nay, naz) : mk(nbx, nby, nbz);
+        }
         bool pass = false;
-        if (lane < n) pass = tri_edges_at<LDS>(S, ws, wp);
+        if (lane < n) pass = tri_edges_at<LDS>(S, ws, wn, wp);
         const unsigned long long r = __ballot(pass);
         oka = na & (((r >> ja) & 1ull) != 0ull);
         okb = nb & (((r >> jb) & 1ull) != 0ull);
     } else {
-        if (na) oka = tri_edges<LDS>(S, s0, o, d, ta);
-        if (nb) okb = tri_edges<LDS>(S, s0 + 1, o, d, tb);
+        if (na) oka = tri_edges_at<LDS>(S, s0, na3, o + d * ta);
+        if (nb) okb = tri_edges_at<LDS>(S, s0 + 1, nb3, o + d * tb);
     }
     h1 = oka ? ta : -1.0f;
     h2 = okb ? tb : -1.0f;
@@ -784,14 +794,14 @@ __device__ __forceinline__ bool collide_ww(const SceneView& S, int n_nodes, int 
         if (!__any(pend)) break;
         if (pend) {
             if (COUNT) { c.tri += 2; diag_tick(c.lw, c.ll); }
-            const float4* T0 = S.tris + 8 * (leaf >> 1);
+            const float4* T0 = S.tris + 8 * (leaf >> 2);
             f3 n0, n1;
             float h1, h2;
             if (flags & PT_FLAG_MOLLER_TRUMBORE) {
-                n0 = mk(T0[0].w, T0[1].w, T0[2].w);
-                n1 = mk(T0[4].w, T0[5].w, T0[6].w);
-                h1 = tri_mt(T0[0], T0[1], T0[2], o, d);
-                h2 = tri_mt(T0[4], T0[5], T0[6], o, d);
+                n0 = mk(T0[0].x, T0[0].y, T0[0].z);
+                n1 = mk(T0[4].x, T0[4].y, T0[4].z);
+                h1 = tri_mt(T0[1], T0[2], T0[3], o, d);
+                h2 = tri_mt(T0[5], T0[6], T0[7], o, d);
             } else {
                 h1 = tri_hit_bf(T0, o, d, t, n0);
                 h2 = tri_hit_bf(T0 + 4, o, d, t, n1);   // single-tri leaves hold a copy
@@ -806,7 +816,7 @@ __device__ __forceinline__ bool collide_ww(const SceneView& S, int n_nodes, int 
                 t = th;
                 normal = nn;
                 hitp = o + d * th;
-                mat = __float_as_int(T0[c1 ? 3 : 7].y);
+                mat = __float_as_int(T0[c1 ? 2 : 6].w);
             }
             pend = false;
         }
@@ -1175,9 +1185,9 @@ __global__ __launch_bounds__(256, MINW) void k_render_sm(KParams p) {
                     f3 normal;
                     int mat;
                     if (hprim >= 0) {             // triangle: stored n, flipped (:421-428)
-                        normal = mk(tri_quad<LDS>(S, hprim, 0).w, tri_quad<LDS>(S, hprim, 1).w,
-                                    tri_quad<LDS>(S, hprim, 2).w);
-                        mat = __float_as_int(tri_quad<LDS>(S, hprim, 3).y);
+                        const float4 nq = tri_quad<LDS>(S, hprim, 0);
+                        normal = mk(nq.x, nq.y, nq.z);
+                        mat = __float_as_int(tri_quad<LDS>(S, hprim, 2).w);
                     } else {                      // sphere: normalize(hit - center) (:380)
                         const int si = -2 - hprim;
                         float4 s0 = S.spheres[2 * si];
@@ -1391,30 +1401,32 @@ __global__ __launch_bounds__(256, MINW) void k_render_sm(KParams p) {
             // ---------------- LEAF: both triangle tests + the 2-way choice (:406-429)
             const bool at = st == ST_LEAF;
             int s0 = 0, cont = -1;
-            float4 q3 = make_float4(0, 0, 0, 0);
+            bool cop = false;
+            float4 nd0 = make_float4(0, 0, 0, 0);
             if (at) {
                 if (COUNT) { c.tri += 2; diag_tick(c.lw, c.ll); }
-                const int code = LDS ? leaf : ~leaf;         // (slot << 1) | single
-                s0 = code & ~1;                              // slots 2k, 2k+1
-                q3 = tri_quad<LDS>(S, s0, 3);                // .z / .w: the leaf's next-right
-                cont = LDS ? __float_as_int(q3.z) : bi;      // LDS: offset in image 0
+                const int code = LDS ? leaf : ~leaf;         // k << 2 | coplanar << 1 | single
+                s0 = (code >> 1) & ~1;                       // slots 2k, 2k+1
+                cop = (code & 2) != 0;
+                nd0 = tri_quad<LDS>(S, s0, 0);               // {n, d0} of the first triangle
+                cont = LDS ? __float_as_int(tri_quad<LDS>(S, s0, 1).w) : bi;   // LDS: next-right, image 0
                 if (LDS && (fast & (cont >= 0))) cont += oct_base(d, S.np << 5);
             }
             float h1 = -1.0f, h2 = -1.0f;
             if (p.flags & PT_FLAG_MOLLER_TRUMBORE) {   // wave-uniform
                 if (at) {
-                    h1 = tri_mt(tri_quad<LDS>(S, s0, 0), tri_quad<LDS>(S, s0, 1), tri_quad<LDS>(S, s0, 2), o, d);
-                    h2 = tri_mt(tri_quad<LDS>(S, s0 + 1, 0), tri_quad<LDS>(S, s0 + 1, 1),
-                                tri_quad<LDS>(S, s0 + 1, 2), o, d);
+                    h1 = tri_mt(tri_quad<LDS>(S, s0, 1), tri_quad<LDS>(S, s0, 2), tri_quad<LDS>(S, s0, 3), o, d);
+                    h2 = tri_mt(tri_quad<LDS>(S, s0 + 1, 1), tri_quad<LDS>(S, s0 + 1, 2),
+                                tri_quad<LDS>(S, s0 + 1, 3), o, d);
                 }
             } else {
 #if PT_LEAF_COMPACT
-                leaf_pair_tests<LDS>(S, at, s0, q3, o, d, t, p.compact_max, h1, h2);
+                leaf_pair_tests<LDS>(S, at, s0, nd0, cop, o, d, t, p.compact_max, h1, h2);
 #else
                 if (at) {
                     f3 n0, n1;
-                    h1 = tri_hit_lazy<LDS>(S, s0, q3, o, d, t, n0);
-                    h2 = tri_hit_lazy<LDS>(S, s0 + 1, tri_quad<LDS>(S, s0 + 1, 3), o, d, t, n1);
+                    h1 = tri_hit_lazy<LDS>(S, s0, nd0, o, d, t, n0);
+                    h2 = tri_hit_lazy<LDS>(S, s0 + 1, tri_quad<LDS>(S, s0 + 1, 0), o, d, t, n1);
                 }
 #endif
             }
@@ -1646,19 +1658,19 @@ __device__ __forceinline__ bool wf_leaf_batch(const KParams& p, const SceneView&
     float t = a0.w;
     int hprim = __float_as_int(a1.w);
     const bool fast = a2.x != 0.0f;
-    const int code = at ? -2 - __float_as_int(a2.w) : 0;    // (slot << 1) | single
-    const int s0 = code & ~1;
-    const float4 q3 = tri_quad<true>(S, s0, 3);
-    int cont = __float_as_int(q3.z);                          // next-right, image-0 offset
+    const int code = at ? -2 - __float_as_int(a2.w) : 0;    // k << 2 | coplanar << 1 | single
+    const int s0 = (code >> 1) & ~1;
+    const float4 nd0 = tri_quad<true>(S, s0, 0);
+    int cont = __float_as_int(tri_quad<true>(S, s0, 1).w);    // next-right, image-0 offset
     if (fast & (cont >= 0)) cont += oct_base(d, S.np << 5);
     float h1 = -1.0f, h2 = -1.0f;
     if (p.flags & PT_FLAG_MOLLER_TRUMBORE) {
         if (at) {
-            h1 = tri_mt(tri_quad<true>(S, s0, 0), tri_quad<true>(S, s0, 1), tri_quad<true>(S, s0, 2), o, d);
-            h2 = tri_mt(tri_quad<true>(S, s0 + 1, 0), tri_quad<true>(S, s0 + 1, 1), tri_quad<true>(S, s0 + 1, 2), o, d);
+            h1 = tri_mt(tri_quad<true>(S, s0, 1), tri_quad<true>(S, s0, 2), tri_quad<true>(S, s0, 3), o, d);
+            h2 = tri_mt(tri_quad<true>(S, s0 + 1, 1), tri_quad<true>(S, s0 + 1, 2), tri_quad<true>(S, s0 + 1, 3), o, d);
         }
     } else {
-        leaf_pair_tests<true>(S, at, s0, q3, o, d, t, p.compact_max, h1, h2);
+        leaf_pair_tests<true>(S, at, s0, nd0, (code & 2) != 0, o, d, t, p.compact_max, h1, h2);
     }
     if (at) {
         const bool c1 = (h1 > 0.0001f) & (h1 < t) & ((h1 < h2) | (h2 < 0.0001f));
@@ -1717,8 +1729,9 @@ __device__ __forceinline__ bool wf_shade_batch(const KParams& p, const SceneView
             f3 normal;
             int mat;
             if (hprim >= 0) {
-                normal = mk(tri_quad<true>(S, hprim, 0).w, tri_quad<true>(S, hprim, 1).w, tri_quad<true>(S, hprim, 2).w);
-                mat = __float_as_int(tri_quad<true>(S, hprim, 3).y);
+                const float4 nq = tri_quad<true>(S, hprim, 0);
+                normal = mk(nq.x, nq.y, nq.z);
+                mat = __float_as_int(tri_quad<true>(S, hprim, 2).w);
             } else {
                 const int sph = -2 - hprim;
                 const float4 c0 = S.spheres[2 * sph];
@@ -2315,12 +2328,12 @@ int pt_upload_scene(pt_ctx* c, const float* tris, int n_tris, const float* bvh, 
         f3 n = pt::normalize(pt::cross(v1 - v0, v2 - v0));
         float d0 = -pt::dot(n, v0);
         int m = (int)t[12];
-        q[0] = make_float4(v0.x, v0.y, v0.z, n.x);
-        q[1] = make_float4(v1.x, v1.y, v1.z, n.y);
-        q[2] = make_float4(v2.x, v2.y, v2.z, n.z);
         float mb;
         std::memcpy(&mb, &m, 4);
-        q[3] = make_float4(d0, mb, 0.0f, 0.0f);
+        q[0] = make_float4(n.x, n.y, n.z, d0);      // the plane test reads this quad alone
+        q[1] = make_float4(v0.x, v0.y, v0.z, 0.0f); // .w: the LDS walk's continuation (below)
+        q[2] = make_float4(v1.x, v1.y, v1.z, mb);
+        q[3] = make_float4(v2.x, v2.y, v2.z, 0.0f);
     };
     for (int i = 0; i < n_nodes; i++) {
         const float* nd = bvh + 12 * (size_t)i;
@@ -2330,20 +2343,19 @@ int pt_upload_scene(pt_ctx* c, const float* tris, int n_tris, const float* bvh, 
             int t0 = (int)nd[8], t1 = (int)nd[9];
             put_tri(&dt[8 * (size_t)s], t0);
             put_tri(&dt[8 * (size_t)s + 4], t1);
+            bool cop;
             {   // coplanar pair: both triangles carry the same (n, d0) up to the sign of zero
                 // components (the two halves of an OBJ quad, a single-triangle leaf's copy),
-                // flagged in the first slot's quad 3 .w.  hit_triangle's plane distance
+                // flagged in the leaf code (bit 1).  hit_triangle's plane distance
                 // -(dot(n,o) + d0) / dot(n,d) is then the same for both wherever it can pass
                 // the leaf's acceptance tests: a zero factor of either sign only changes the
                 // sign of zero intermediate sums, so the two quotients are bitwise equal or
                 // both +-0, +-inf or NaN, which fail t > 1e-4 / t >= 1e-4 alike.  NaN (a
                 // degenerate triangle) never compares equal: such pairs are not flagged.
-                const float4* A = &dt[8 * (size_t)s];
-                const float4* B = A + 4;
-                const bool cop = A[0].w == B[0].w && A[1].w == B[1].w && A[2].w == B[2].w && A[3].x == B[3].x;
-                dt[8 * (size_t)s + 3].w = cop ? 1.0f : 0.0f;
+                const float4 A = dt[8 * (size_t)s], B = dt[8 * (size_t)s + 4];
+                cop = A.x == B.x && A.y == B.y && A.z == B.z && A.w == B.w;
             }
-            a = ~((s << 1) | (t0 == t1 ? 1 : 0));
+            a = ~((s << 2) | (cop ? 2 : 0) | (t0 == t1 ? 1 : 0));
             b = (int)nd[11];
             slot_of[pos[i]] = s;
         } else {
@@ -2379,7 +2391,7 @@ int pt_upload_scene(pt_ctx* c, const float* tris, int n_tris, const float* bvh, 
     // LDS walk images of the state-machine kernel (WalkLinks in the kernel source): per ray
     // octant k the node planes (bounds of the axes whose bit is set in k swapped) with links
     // as byte offsets (16 * (2N * k + index)) and a leaf's hit link -2 - code; the leaf's
-    // next-right (image-0 offset) goes to its first triangle's quad 3 .z
+    // next-right (image-0 offset) goes to its first triangle's quad 1 .w
     const size_t N = (size_t)(n_nodes <= kPadNodes ? kPadNodes : n_nodes);   // nodes per image plane
     std::vector<float4> dwl(16 * N, make_float4(0, 0, 0, 0));
     for (int k = 0; k < 8; k++) {
@@ -2398,7 +2410,7 @@ int pt_upload_scene(pt_ctx* c, const float* tris, int n_tris, const float* bvh, 
             if (k & 4) std::swap(hi.x, hi.y);
             dwl[2 * N * k + i] = lo;
             dwl[2 * N * k + N + i] = hi;
-            if (leaf && k == 0) std::memcpy(&dt[8 * (size_t)slot_of[i] + 3].z, &hb, 4);
+            if (leaf && k == 0) std::memcpy(&dt[8 * (size_t)slot_of[i] + 1].w, &hb, 4);
         }
     }
     HIPCHK(c, hipStreamSynchronize(c->stream));   // a render in flight may still read the old scene
