@@ -85,6 +85,7 @@ struct KParams {
     // wave stops walking to refill, and the queue depths that start a leaf / shade batch
     int wf_paths, wf_ring, wf_refill, wf_leaf_min, wf_shade_min;
     unsigned* wf_err;              // watchdog trips of the wavefront kernel (must stay 0)
+    int shade_lds;                 // global-memory scene: materials + spheres staged in LDS too
 };
 
 // Progressive mode (hipGraph replay): the frame range comes from a device counter, and
@@ -1114,6 +1115,16 @@ __global__ __launch_bounds__(256, MINW) void k_render_sm(KParams p) {
         if ((unsigned)(size_t)(__attribute__((address_space(3))) const char*)g_lds != 0u) __builtin_trap();
         const int K = p.n_top;
         for (int i = threadIdx.x; i < 2 * K; i += blockDim.x) lds[(i & 1) * K + (i >> 1)] = p.sc.nodes[i];
+        // materials and spheres after them when small (p.shade_lds): every segment's sphere
+        // test and every hit's material then read LDS, not scattered global lines (the global
+        // walk is bound by its vector-memory lane-loads)
+        if (p.shade_lds) {
+            const int nm = 3 * p.n_mats, ns = 2 * p.sc.n_spheres;
+            for (int i = threadIdx.x; i < nm; i += blockDim.x) lds[2 * K + i] = p.sc.mats[i];
+            for (int i = threadIdx.x; i < ns; i += blockDim.x) lds[2 * K + nm + i] = p.sc.spheres[i];
+            S.mats = lds + 2 * K;
+            S.spheres = lds + 2 * K + nm;
+        }
         __syncthreads();
         S.np = K;
         S.tp = 0;
@@ -2763,7 +2774,10 @@ static int enqueue_render(pt_ctx* c, int frame_first, int n_frames, int acc_firs
         // global scene: the top nodes staged per block, at most what mw blocks per CU fit in
         // its 160 KiB of LDS (the first K of the breadth-first numbering, any K <= n_top)
         if (mw > 6) p.n_top = std::min(c->n_top, 160 * 1024 / mw / 32 - 8);
-        const size_t top_lds = (size_t)p.n_top * 2 * sizeof(float4);
+        // materials + spheres beside the top nodes when they are small (<= 4 KiB)
+        const size_t shade_bytes = (size_t)(3 * c->n_mats + 2 * c->n_spheres) * sizeof(float4);
+        p.shade_lds = shade_bytes <= 4096;
+        const size_t top_lds = (size_t)p.n_top * 2 * sizeof(float4) + (p.shade_lds ? shade_bytes : 0);
 #define PT_LAUNCH_SM(L, M)                                                                                    \
     if (c->counting && p.rgb) hipLaunchKernelGGL((k_render_sm<true, L, 5, M, true>), grid, dim3(256), L ? lds : top_lds, c->stream, p); \
     else if (c->counting) hipLaunchKernelGGL((k_render_sm<true, L, 5, M, false>), grid, dim3(256), L ? lds : top_lds, c->stream, p); \
