@@ -123,8 +123,8 @@ int pt_stats_ex(pt_ctx* ctx, unsigned long long out[16]);
 int pt_timing(pt_ctx* ctx, double* total_kernel_ms, int* n_launches, int reset);
 
 /* Kernel variant selection (0 = default/fastest); see DESIGN.md §5 for the list.
- * 4 = wavefront queues (experimental): LDS-staged scenes, raysPerPixel 1, no counting;
- * otherwise it runs variant 0. */
+ * 4 = wavefront queues (experimental): raysPerPixel 1, no counting, materials + spheres
+ * within 4 KiB for global-memory scenes; otherwise it runs variant 0. */
 int pt_set_kernel(pt_ctx* ctx, int variant);
 /* Scheduling knobs of the state-machine kernel:
  * key 0 = run the leaf phase once this many lanes wait at leaves (1..64, 0 = auto),
@@ -146,7 +146,8 @@ int pt_set_kernel(pt_ctx* ctx, int variant);
  *         32-bit work-queue ids would overflow -- runs as back-to-back launches, the first
  *         with the caller's accumulate flag and the rest accumulating: the same image.
  * keys 10-14 = variant 4 (wavefront queues): 10 path slots per workgroup (64..1536, 0 = as
- *         many as fit beside the scene), 11 walkers below which a wave refills (0 = 16),
+ *         many as fit beside the scene), 11 walkers below which a wave refills (0 = 16 for
+ *         LDS-staged scenes, 40 for global-memory scenes),
  *         12 / 13 leaf / shade batch minimum (1..64, 0 = 64), 14 threads per workgroup
  *         (512, 768, 896, 1024; 0 = 1024).
  * None of these change the image (each pixel's frames stay in order in one lane). */

@@ -1633,7 +1633,9 @@ __device__ __forceinline__ int wf_pop(const WfLds& L, int q, unsigned long long 
 
 // The walk of the wavefront kernel: the lanes with w >= 0 take node steps (bvh_intersect +
 // the link choice, WalkLinks) until at most `refill` of them still walk.
-template <bool ALL_FAST, bool PADN>
+// LDS scenes walk the octant images (WalkLinks); global-memory scenes the reference links
+// (node indices; a leaf's hit link ~code becomes -2 - code), top nodes from LDS.
+template <bool ALL_FAST, bool LDS, bool PADN>
 __device__ __forceinline__ void wf_walk(const SceneView& S, f3 o, f3 d, f3 rd, bool fast, float t, int refill,
                                         int& w, WfDiag& dg) {
     for (;;) {
@@ -1644,10 +1646,11 @@ __device__ __forceinline__ void wf_walk(const SceneView& S, f3 o, f3 d, f3 rd, b
 #endif
             if (w >= 0) {
                 float4 lo, hi;
-                node_at<true, PADN>(S, w, lo, hi);
+                node_at<LDS, PADN>(S, w, lo, hi);
                 const int a = __float_as_int(hi.z), b = __float_as_int(hi.w);
-                const bool hb = (ALL_FAST || fast) ? slab_oct(lo, hi, o, d, rd, t) : slab(lo, hi, o, d, t);
-                w = hb ? a : b;
+                const bool hb = (ALL_FAST || fast) ? (LDS ? slab_oct(lo, hi, o, d, rd, t) : slab_fast(lo, hi, o, d, rd, t))
+                                                   : slab(lo, hi, o, d, t);
+                w = hb ? (LDS || a >= 0 ? a : a - 1) : b;
             }
         }
         if (__popcll(__ballot(w >= 0)) <= refill) break;
@@ -1656,6 +1659,7 @@ __device__ __forceinline__ void wf_walk(const SceneView& S, f3 o, f3 d, f3 rd, b
 
 // Leaf batch: up to 64 rays from the leaf queue, both triangle tests + the 2-way choice
 // (:406-429), then back to the walk queue at the leaf's continuation (or to the shade queue).
+template <bool LDS>
 __device__ __forceinline__ bool wf_leaf_batch(const KParams& p, const SceneView& S, const WfLds& L, WfDiag& dg,
                                               bool strict) {
     const int s = wf_pop(L, kWfQL, ~0ull, p.wf_err, dg, strict);
@@ -1671,17 +1675,19 @@ __device__ __forceinline__ bool wf_leaf_batch(const KParams& p, const SceneView&
     const bool fast = a2.x != 0.0f;
     const int code = at ? -2 - __float_as_int(a2.w) : 0;    // k << 2 | coplanar << 1 | single
     const int s0 = (code >> 1) & ~1;
-    const float4 nd0 = tri_quad<true>(S, s0, 0);
-    int cont = __float_as_int(tri_quad<true>(S, s0, 1).w);    // next-right, image-0 offset
-    if (fast & (cont >= 0)) cont += oct_base(d, S.np << 5);
+    const float4 nd0 = tri_quad<LDS>(S, s0, 0);
+    // the leaf's next-right: LDS image-0 byte offset (quad 1 .w, + the ray's octant image) or
+    // global node index (quad 3 .w)
+    int cont = __float_as_int(tri_quad<LDS>(S, s0, LDS ? 1 : 3).w);
+    if (LDS && (fast & (cont >= 0))) cont += oct_base(d, S.np << 5);
     float h1 = -1.0f, h2 = -1.0f;
     if (p.flags & PT_FLAG_MOLLER_TRUMBORE) {
         if (at) {
-            h1 = tri_mt(tri_quad<true>(S, s0, 1), tri_quad<true>(S, s0, 2), tri_quad<true>(S, s0, 3), o, d);
-            h2 = tri_mt(tri_quad<true>(S, s0 + 1, 1), tri_quad<true>(S, s0 + 1, 2), tri_quad<true>(S, s0 + 1, 3), o, d);
+            h1 = tri_mt(tri_quad<LDS>(S, s0, 1), tri_quad<LDS>(S, s0, 2), tri_quad<LDS>(S, s0, 3), o, d);
+            h2 = tri_mt(tri_quad<LDS>(S, s0 + 1, 1), tri_quad<LDS>(S, s0 + 1, 2), tri_quad<LDS>(S, s0 + 1, 3), o, d);
         }
     } else {
-        leaf_pair_tests<true>(S, at, s0, nd0, (code & 2) != 0, o, d, t, p.compact_max, h1, h2);
+        leaf_pair_tests<LDS>(S, at, s0, nd0, (code & 2) != 0, o, d, t, p.compact_max, h1, h2);
     }
     if (at) {
         const bool c1 = (h1 > 0.0001f) & (h1 < t) & ((h1 < h2) | (h2 < 0.0001f));
@@ -1704,6 +1710,7 @@ __device__ __forceinline__ bool wf_leaf_batch(const KParams& p, const SceneView&
 // (next frame of the work item, or a new item from the device queue), sets up the next
 // segment (guard, spheres :372-385, walk start) and queues it.  The operations are those of
 // k_render_sm's SHADE phase for one path.
+template <bool LDS>
 __device__ __forceinline__ bool wf_shade_batch(const KParams& p, const SceneView& S, const WfLds& L,
                                                unsigned total_ids, unsigned n_groups, int root_skip, WfDiag& dg,
                                                bool strict) {
@@ -1740,9 +1747,9 @@ __device__ __forceinline__ bool wf_shade_batch(const KParams& p, const SceneView
             f3 normal;
             int mat;
             if (hprim >= 0) {
-                const float4 nq = tri_quad<true>(S, hprim, 0);
+                const float4 nq = tri_quad<LDS>(S, hprim, 0);
                 normal = mk(nq.x, nq.y, nq.z);
-                mat = __float_as_int(tri_quad<true>(S, hprim, 2).w);
+                mat = __float_as_int(tri_quad<LDS>(S, hprim, 2).w);
             } else {
                 const int sph = -2 - hprim;
                 const float4 c0 = S.spheres[2 * sph];
@@ -1925,7 +1932,7 @@ __device__ __forceinline__ bool wf_shade_batch(const KParams& p, const SceneView
         const bool inside = (root_skip >= 0) & fast & (o.x >= p.root_box[0]) & (o.x <= p.root_box[1]) &
                             (o.y >= p.root_box[2]) & (o.y <= p.root_box[3]) & (o.z >= p.root_box[4]) &
                             (o.z <= p.root_box[5]);
-        const int img = fast ? oct_base(d, S.np << 5) : 0;
+        const int img = (LDS && fast) ? oct_base(d, S.np << 5) : 0;
         w = walk ? (inside ? root_skip : 0) + img : -1;
         flags = 0u;                // a segment is set up: the next batch finishes it
     }
@@ -1947,25 +1954,33 @@ __device__ __forceinline__ bool wf_shade_batch(const KParams& p, const SceneView
 }
 
 // NT threads per workgroup; MINW = resident waves per SIMD (the register budget)
-template <bool PADN, int NT, int MINW>
+// LDS: the scene staged as in k_render_sm; !LDS (global-memory scene): the top p.n_top
+// nodes, the materials and the spheres in LDS, nodes below and the triangles in global
+// memory.  The path records follow in either case.
+template <bool LDS, bool PADN, int NT, int MINW>
 __global__ __launch_bounds__(NT, MINW) void k_render_wf(KParams p) {
     resolve_frames(p);
     extern __shared__ float4 lds[];
     if ((unsigned)(size_t)(__attribute__((address_space(3))) const char*)g_lds != 0u) __builtin_trap();
-    const int N = PADN ? kPadNodes : p.walk_np, T = p.n_slots, nn = 16 * N, nt = 4 * T;
+    const int N = LDS ? (PADN ? kPadNodes : p.walk_np) : p.n_top, T = p.n_slots;
+    const int nn = LDS ? 16 * N : 2 * N, nt = LDS ? 4 * T : 0;
     const int nm = 3 * p.n_mats, ns = 2 * p.sc.n_spheres;
     const int tid = threadIdx.x;
-    for (int i = tid; i < nn; i += NT) lds[i] = p.sc.walk_lds[i];
-    for (int i = tid; i < nt; i += NT) lds[nn + (i & 3) * T + (i >> 2)] = p.sc.tris[i];
+    if (LDS) {
+        for (int i = tid; i < nn; i += NT) lds[i] = p.sc.walk_lds[i];
+        for (int i = tid; i < nt; i += NT) lds[nn + (i & 3) * T + (i >> 2)] = p.sc.tris[i];
+    } else {   // top nodes in planes: lo at [i], hi at [N + i]
+        for (int i = tid; i < nn; i += NT) lds[(i & 1) * N + (i >> 1)] = p.sc.nodes[i];
+    }
     for (int i = tid; i < nm; i += NT) lds[nn + nt + i] = p.sc.mats[i];
     for (int i = tid; i < ns; i += NT) lds[nn + nt + nm + i] = p.sc.spheres[i];
     SceneView S;
-    S.nodes = lds;
-    S.tris = lds + nn;
+    S.nodes = LDS ? lds : p.sc.nodes;
+    S.tris = LDS ? lds + nn : p.sc.tris;
     S.mats = lds + nn + nt;
     S.spheres = lds + nn + nt + nm;
     S.np = N;
-    S.tp = T;
+    S.tp = LDS ? T : 0;
     const int P = p.wf_paths;
     WfLds L;
     L.r0 = nn + nt + nm + ns;
@@ -1995,7 +2010,7 @@ __global__ __launch_bounds__(NT, MINW) void k_render_wf(KParams p) {
     const int tiles_x = (p.W + 7) >> 3;
     const unsigned n_groups = (unsigned)((p.n_frames + p.group - 1) / p.group);
     const unsigned total_ids = (unsigned)tiles_x * (unsigned)((p.rows_local + 7) >> 3) * n_groups * 64u;
-    const int root_skip = p.root_child < 0 ? -1 : p.root_child << 4;
+    const int root_skip = p.root_child < 0 ? -1 : p.root_child << (LDS ? 4 : 0);
 
     // the wave's walkers (w < 0: lane free, slot -1 once its ray is queued)
     int slot = -1, w = -1;
@@ -2013,9 +2028,9 @@ __global__ __launch_bounds__(NT, MINW) void k_render_wf(KParams p) {
     for (;;) {
         const unsigned aL = wf_peek(L, 3 * kWfQL + 2), aS = wf_peek(L, 3 * kWfQS + 2);
         // full batches (all 64 lanes, or none when another wave took them first)
-        if ((int)aL >= p.wf_leaf_min && wf_leaf_batch(p, S, L, dg, p.wf_leaf_min >= 64)) { idle_t0 = 0; WF_CLK(8); continue; }
+        if ((int)aL >= p.wf_leaf_min && wf_leaf_batch<LDS>(p, S, L, dg, p.wf_leaf_min >= 64)) { idle_t0 = 0; WF_CLK(8); continue; }
         if ((int)aS >= p.wf_shade_min &&
-            wf_shade_batch(p, S, L, total_ids, n_groups, root_skip, dg, p.wf_shade_min >= 64)) {
+            wf_shade_batch<LDS>(p, S, L, total_ids, n_groups, root_skip, dg, p.wf_shade_min >= 64)) {
             idle_t0 = 0;
             WF_CLK(9);
             continue;
@@ -2038,8 +2053,8 @@ __global__ __launch_bounds__(NT, MINW) void k_render_wf(KParams p) {
         }
         if (__any(w >= 0)) {
             idle_t0 = 0;
-            if (__all(fast || w < 0)) wf_walk<true, PADN>(S, o, d, rd, fast, t, p.wf_refill, w, dg);
-            else wf_walk<false, PADN>(S, o, d, rd, fast, t, p.wf_refill, w, dg);
+            if (__all(fast || w < 0)) wf_walk<true, LDS, PADN>(S, o, d, rd, fast, t, p.wf_refill, w, dg);
+            else wf_walk<false, LDS, PADN>(S, o, d, rd, fast, t, p.wf_refill, w, dg);
             // stopped rays: at a hit leaf (w <= -2) to the leaf queue, walk ended (-1) to shading
             const bool stopped = (w < 0) & (slot >= 0);
             if (stopped & (w <= -2)) wf_stw(L.r2, slot, __int_as_float(w));
@@ -2050,8 +2065,8 @@ __global__ __launch_bounds__(NT, MINW) void k_render_wf(KParams p) {
             continue;
         }
         // nothing to walk: drain whatever the queues hold, else wait for the other waves
-        if (aL && wf_leaf_batch(p, S, L, dg, false)) { idle_t0 = 0; WF_CLK(8); continue; }
-        if (aS && wf_shade_batch(p, S, L, total_ids, n_groups, root_skip, dg, false)) { idle_t0 = 0; WF_CLK(9); continue; }
+        if (aL && wf_leaf_batch<LDS>(p, S, L, dg, false)) { idle_t0 = 0; WF_CLK(8); continue; }
+        if (aS && wf_shade_batch<LDS>(p, S, L, total_ids, n_groups, root_skip, dg, false)) { idle_t0 = 0; WF_CLK(9); continue; }
         if (wf_peek(L, kWfLive) == 0u) break;
         // watchdog (100 MHz clock): idle for 2 s while paths are live means a lost path;
         // give up (the host reports PT_E_HIP) rather than spin forever
@@ -2374,6 +2389,8 @@ int pt_upload_scene(pt_ctx* c, const float* tris, int n_tris, const float* bvh, 
             b = (int)nd[11];
         }
         if (b >= 0) b = pos[b];
+        if (leaf_slot[i] >= 0)     // global-memory walks of variant 4: the leaf's next-right
+            std::memcpy(&dt[8 * (size_t)leaf_slot[i] + 3].w, &b, 4);
         float fa, fb;
         std::memcpy(&fa, &a, 4);
         std::memcpy(&fb, &b, 4);
@@ -2612,13 +2629,22 @@ static int ensure_rgb(pt_ctx* c, int n_frames) {
 // Otherwise variant 4 falls back to the state-machine kernel (variant 0).  Returns the path
 // slots per workgroup, 0 when variant 4 does not run.
 static int wf_threads(const pt_ctx* c) { return c->wf_threads ? c->wf_threads : 1024; }
+// LDS bytes of variant 4's scene part: an LDS-staged scene as variant 0 stages it; for a
+// global-memory scene the top nodes plus materials and spheres (-1: these do not fit).
+static long long wf_scene_bytes(const pt_ctx* c) {
+    if (c->lds_bytes <= kLdsSceneMax) return (long long)c->lds_bytes;
+    const long long shade = (3LL * c->n_mats + 2LL * c->n_spheres) * 16;
+    if (shade > 4096) return -1;
+    return (long long)c->n_top * 32 + shade;
+}
 static int wf_paths(const pt_ctx* c, int n_frames) {
     if (c->variant != 4 || c->counting || c->cfg.rays_per_pixel != 1 || c->cfg.max_bounce > 250 || n_frames > 65535)
         return 0;
-    if (c->lds_bytes > kLdsSceneMax) return 0;
+    const long long scene = wf_scene_bytes(c);
+    if (scene < 0) return 0;
     const int per_cu = wf_threads(c) <= 512 ? 4 : (wf_threads(c) < 1024 ? 2 : 1);   // workgroups per CU
     // 96 B of records per path slot plus 3 ring entries (2 B, rings of at most 2x the slots)
-    const long long room = 160 * 1024 / per_cu - (long long)c->lds_bytes - 64;
+    const long long room = 160 * 1024 / per_cu - scene - 64;
     const int fit = (int)std::min<long long>(room / (96 + 12), 1536);
     const int P = c->wf_paths ? std::min(c->wf_paths, fit) : fit;
     return P >= 64 ? P : 0;
@@ -2730,10 +2756,12 @@ static int enqueue_render(pt_ctx* c, int frame_first, int n_frames, int acc_firs
         p.wf_ring = 64;
         while (p.wf_ring < wfP) p.wf_ring <<= 1;
         p.wf_err = c->d_work + 4;            // reset with the queue counter below
-        p.wf_refill = c->wf_refill ? c->wf_refill : 16;     // keysweep: 16 +4% over 40
+        // keysweep: LDS scenes 16 (+4% over 40), global-memory scenes 40 (+15% over 16)
+        p.wf_refill = c->wf_refill ? c->wf_refill : (c->lds_bytes <= kLdsSceneMax ? 16 : 40);
         p.wf_leaf_min = c->wf_leaf_min ? c->wf_leaf_min : 64;
         p.wf_shade_min = c->wf_shade_min ? c->wf_shade_min : 64;
-        const size_t lds = c->lds_bytes + 96 * (size_t)wfP + 3 * (size_t)p.wf_ring * 2 + 64;
+        const size_t lds = (size_t)wf_scene_bytes(c) + 96 * (size_t)wfP + 3 * (size_t)p.wf_ring * 2 + 64;
+        const bool wl = c->lds_bytes <= kLdsSceneMax;      // LDS-staged scene (else global)
         const unsigned long long ids = (unsigned long long)c->n_tiles * 64ull *
                                        (unsigned long long)((n_frames + p.group - 1) / p.group);
         const int nt = wf_threads(c);
@@ -2741,8 +2769,9 @@ static int enqueue_render(pt_ctx* c, int frame_first, int n_frames, int acc_firs
         const unsigned grid = (unsigned)std::min<unsigned long long>(
             (unsigned long long)c->n_cu * per_cu, std::max(1ull, (ids + wfP - 1) / (unsigned long long)wfP));
 #define PT_WF(NT)                                                                                             \
-    if (c->walk_np == kPadNodes) hipLaunchKernelGGL((k_render_wf<true, NT, NT / 64 * (NT <= 512 ? 4 : (NT < 1024 ? 2 : 1)) / 4>), dim3(grid), dim3(NT), lds, c->stream, p); \
-    else hipLaunchKernelGGL((k_render_wf<false, NT, NT / 64 * (NT <= 512 ? 4 : (NT < 1024 ? 2 : 1)) / 4>), dim3(grid), dim3(NT), lds, c->stream, p);
+    if (!wl) hipLaunchKernelGGL((k_render_wf<false, false, NT, NT / 64 * (NT <= 512 ? 4 : (NT < 1024 ? 2 : 1)) / 4>), dim3(grid), dim3(NT), lds, c->stream, p); \
+    else if (c->walk_np == kPadNodes) hipLaunchKernelGGL((k_render_wf<true, true, NT, NT / 64 * (NT <= 512 ? 4 : (NT < 1024 ? 2 : 1)) / 4>), dim3(grid), dim3(NT), lds, c->stream, p); \
+    else hipLaunchKernelGGL((k_render_wf<true, false, NT, NT / 64 * (NT <= 512 ? 4 : (NT < 1024 ? 2 : 1)) / 4>), dim3(grid), dim3(NT), lds, c->stream, p);
         if (nt == 512) { PT_WF(512) }
         else if (nt == 768) { PT_WF(768) }
         else if (nt == 896) { PT_WF(896) }

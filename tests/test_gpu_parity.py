@@ -177,7 +177,7 @@ def big_scene(request, tmp_path_factory):
     return H.setupBuffers(*pt_scenes.write_scene(request.param, d))
 
 
-@pytest.mark.parametrize("variant", [0, 2])
+@pytest.mark.parametrize("variant", [0, 2, 4])
 def test_large_scene_bitwise(big_scene, variant):
     """C3/C4 stand-ins (69k / 249k triangles): the scene no longer fits the LDS staging
     budget, so the kernels walk the BVH from global memory."""
@@ -492,3 +492,22 @@ def test_wavefront_full_hd_sampled(cornell_scene):
     pt.close()
     want = O.render_pixels(cornell_scene, W, Hh, xs, ys, max_bounce=8, n_frames=6)
     assert_bitwise(img[ys, xs], want, "wavefront 1080p")
+
+
+@pytest.mark.parametrize("paths,refill", [(0, 0), (64, 64), (300, 1)])
+def test_wavefront_global_scene_bitwise(big_scene, paths, refill):
+    """Variant 4 on a global-memory scene (top nodes in LDS, the rest and the triangles in
+    global memory, continuations from the triangle slots): few or many path slots, refill
+    after every walk batch or only when the wave runs dry; frame offset and prior image."""
+    prior = np.random.default_rng(8).random((27, 48, 4), dtype=np.float32)
+    want = O.render(big_scene, 48, 27, max_bounce=8, frame_first=5, n_frames=3, acc_first=1, accum=prior.copy())
+    pt = H.PathTracer(48, 27, max_bounce=8)
+    pt.set_kernel(4)
+    pt.set_key(10, paths)
+    pt.set_key(11, refill)
+    pt.upload(big_scene)
+    pt.write_rgba32f(prior)
+    pt.render(5, 3, 1)
+    got = pt.read_rgba32f()
+    pt.close()
+    assert_bitwise(got, want, "wavefront global %d/%d" % (paths, refill))
