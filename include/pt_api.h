@@ -67,6 +67,9 @@ int pt_upload_scene(pt_ctx* ctx, const float* tris, int n_tris, const float* bvh
 
 /* cam: 12 floats {position.xyzw, direction.xyzw, data.xyzw} (computeShader.c:50-55). */
 int pt_set_camera(pt_ctx* ctx, const float cam[12]);
+/* Uniform displayMode (1..4), set per frame by the reference (ogl_path_trace.h:182; the
+ * keys 1-4 change it, :261-265).  Replaces pt_config.display_mode for later renders. */
+int pt_set_display_mode(pt_ctx* ctx, int display_mode);
 
 /* Equivalent to n_frames reference dispatches with frame = frame_first .. frame_first+n-1;
  * only the first uses accumulate = accumulate_first, the rest accumulate = 1 (running

@@ -11,11 +11,14 @@
 // ACES-tonemapped RGBA8 view as binary PPM (screenQuadFrag.c).
 #include "../../include/pt_api.h"
 #include "../../include/pt_scene.h"
+#include "../../include/pt_viewer.h"
 
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <fstream>
+#include <sstream>
 #include <string>
 #include <vector>
 
@@ -23,9 +26,77 @@ static void usage() {
     std::fprintf(stderr,
                  "usage: ptrace <scene.obj> <scene.mtl | -> [--width W] [--height H] [--spp S] [--chunk C]\n"
                  "              [--bounces B] [--mode 1..4] [--gpus G] [--pfm out.pfm] [--ppm out.ppm]\n"
-                 "              [--camera px py pz dx dy dz] [--robust]\n"
+                 "              [--camera px py pz dx dy dz] [--robust] [--events script.txt]\n"
                  "  --robust  general Wavefront ingest (v/vt/vn corners, polygons, negative indices,\n"
-                 "            free-form MTL; '-' as the MTL uses the OBJ's mtllib)\n");
+                 "            free-form MTL; '-' as the MTL uses the OBJ's mtllib)\n"
+                 "  --events  replay a recorded interactive session instead of --spp frames: the\n"
+                 "            reference's render loop with its camera controller and accumulation\n"
+                 "            reset (include/pt_viewer.h).  Script lines:\n"
+                 "              frame T            one loop iteration at glfwGetTime() = T seconds\n"
+                 "              frames N T0 DT     N iterations at T0, T0+DT, ...\n"
+                 "              key K ACTION       key callback; K = GLFW code or w a s d 1-4 space shift esc,\n"
+                 "                                 ACTION = press | release | repeat\n"
+                 "              cursor X Y         cursor callback\n"
+                 "            '#' starts a comment; the loop ends early once esc was pressed\n");
+}
+
+// One event of an --events script (see usage()).
+struct Event {
+    int kind;          // 0 frame, 1 key, 2 cursor
+    double a, b;
+    int key, action;
+};
+
+static bool parse_events(const char* path, std::vector<Event>& ev, std::string& err) {
+    std::ifstream in(path);
+    if (!in) { err = std::string("cannot open ") + path; return false; }
+    std::string line;
+    int ln = 0;
+    while (std::getline(in, line)) {
+        ln++;
+        const size_t hash = line.find('#');
+        if (hash != std::string::npos) line.resize(hash);
+        std::istringstream ss(line);
+        std::string op;
+        if (!(ss >> op)) continue;
+        Event e = {0, 0.0, 0.0, 0, 0};
+        bool ok = true;
+        if (op == "frame") {
+            ok = static_cast<bool>(ss >> e.a);
+            ev.push_back(e);
+        } else if (op == "frames") {
+            long n = 0;
+            double t0 = 0, dt = 0;
+            ok = static_cast<bool>(ss >> n >> t0 >> dt) && n >= 0;
+            for (long i = 0; ok && i < n; i++) { e.a = t0 + (double)i * dt; ev.push_back(e); }
+        } else if (op == "key") {
+            std::string k, a;
+            ok = static_cast<bool>(ss >> k >> a);
+            e.kind = 1;
+            if (k == "w" || k == "W") e.key = PT_KEY_W;
+            else if (k == "a" || k == "A") e.key = PT_KEY_A;
+            else if (k == "s" || k == "S") e.key = PT_KEY_S;
+            else if (k == "d" || k == "D") e.key = PT_KEY_D;
+            else if (k == "space") e.key = PT_KEY_SPACE;
+            else if (k == "shift") e.key = PT_KEY_LEFT_SHIFT;
+            else if (k == "esc") e.key = PT_KEY_ESCAPE;
+            else if (k.size() == 1 && k[0] >= '1' && k[0] <= '4') e.key = PT_KEY_1 + (k[0] - '1');
+            else e.key = std::atoi(k.c_str());
+            if (a == "press") e.action = PT_PRESS;
+            else if (a == "release") e.action = PT_RELEASE;
+            else if (a == "repeat") e.action = PT_REPEAT;
+            else e.action = std::atoi(a.c_str());
+            ev.push_back(e);
+        } else if (op == "cursor") {
+            e.kind = 2;
+            ok = static_cast<bool>(ss >> e.a >> e.b);
+            ev.push_back(e);
+        } else {
+            ok = false;
+        }
+        if (!ok) { err = std::string(path) + ":" + std::to_string(ln) + ": bad event line"; return false; }
+    }
+    return true;
 }
 
 #define CHECK(expr, ctx)                                                              \
@@ -45,6 +116,7 @@ int main(int argc, char** argv) {
     std::string pfm = "out.pfm", ppm = "out.ppm";
     float cam[12] = {0, -6, 1, 0, 0, 1, 0, 0, 0, 0, 0, 0};                          // ogl_path_trace.h:53-54
     bool robust = false;
+    const char* events = nullptr;
     for (int i = 3; i < argc; i++) {
         std::string a = argv[i];
         auto next = [&](void) -> const char* { if (i + 1 >= argc) { usage(); std::exit(2); } return argv[++i]; };
@@ -59,6 +131,7 @@ int main(int argc, char** argv) {
         else if (a == "--ppm") ppm = next();
         else if (a == "--camera") { for (int k = 0; k < 6; k++) cam[k < 3 ? k : k + 1] = (float)std::atof(next()); }
         else if (a == "--robust") robust = true;
+        else if (a == "--events") events = next();
         else { usage(); return 2; }
     }
     if (spp < 1 || chunk < 1 || gpus < 1) { usage(); return 2; }
@@ -91,12 +164,41 @@ int main(int argc, char** argv) {
         CHECK(pt_set_camera(ctx[g], cam), ctx[g]);
     }
     auto t1 = std::chrono::steady_clock::now();
-    for (int f0 = 1; f0 <= spp; f0 += chunk) {
-        int n = std::min(chunk, spp - f0 + 1);
-        for (int g = 0; g < gpus; g++) CHECK(pt_render_async(ctx[g], f0, n, f0 == 1 ? 0 : 1), ctx[g]);
+    int frames_run = 0, resets = 0;
+    if (events) {
+        // the reference's render loop (ogl_path_trace.h:160-204) driven by a recorded session
+        std::vector<Event> ev;
+        std::string err;
+        if (!parse_events(events, ev, err)) { std::fprintf(stderr, "%s\n", err.c_str()); return 2; }
+        pt_viewer* view = nullptr;
+        if (pt_viewer_create(cam, mode, &view)) { std::fprintf(stderr, "pt_viewer_create failed\n"); return 1; }
+        for (const Event& e : ev) {
+            if (e.kind == 1) pt_viewer_key(view, e.key, e.action);
+            else if (e.kind == 2) pt_viewer_cursor(view, e.a, e.b);
+            else {
+                if (pt_viewer_should_close(view)) break;     // glfwWindowShouldClose (:160)
+                pt_viewer_frame_info fi;
+                pt_viewer_next(view, e.a, &fi);
+                for (int g = 0; g < gpus; g++) {
+                    CHECK(pt_set_display_mode(ctx[g], fi.display_mode), ctx[g]);
+                    CHECK(pt_set_camera(ctx[g], fi.camera), ctx[g]);
+                    CHECK(pt_render_async(ctx[g], fi.frame, 1, fi.accumulate), ctx[g]);
+                }
+                frames_run++;
+                resets += fi.accumulate == 0;
+            }
+        }
+        pt_viewer_destroy(view);
+        spp = frames_run;
+    } else {
+        for (int f0 = 1; f0 <= spp; f0 += chunk) {
+            int n = std::min(chunk, spp - f0 + 1);
+            for (int g = 0; g < gpus; g++) CHECK(pt_render_async(ctx[g], f0, n, f0 == 1 ? 0 : 1), ctx[g]);
+        }
     }
     for (int g = 0; g < gpus; g++) CHECK(pt_sync(ctx[g]), ctx[g]);
     double secs = std::chrono::duration<double>(std::chrono::steady_clock::now() - t1).count();
+    if (events) std::printf("replayed %s: %d frames, %d accumulation restarts\n", events, frames_run, resets);
 
     std::vector<float> img(4 * (size_t)W * H, 0.0f);
     std::vector<unsigned char> rgba(4 * (size_t)W * H, 0);
@@ -115,7 +217,7 @@ int main(int argc, char** argv) {
         pt_destroy(ctx[g]);
     }
     std::printf("rendered %dx%d, %d spp, %d bounces on %d GPU(s): %.3f s, %.3f ms/frame\n", W, H, spp, bounces,
-                gpus, secs, secs * 1e3 / spp);
+                gpus, secs, secs * 1e3 / (spp > 0 ? spp : 1));
 
     if (FILE* f = std::fopen(pfm.c_str(), "wb")) {       // PFM rows run bottom-to-top: no flip
         std::fprintf(f, "PF\n%d %d\n-1.0\n", W, H);

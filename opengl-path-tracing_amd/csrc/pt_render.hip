@@ -2502,6 +2502,14 @@ int pt_set_camera(pt_ctx* c, const float cam[12]) {
     return PT_OK;
 }
 
+int pt_set_display_mode(pt_ctx* c, int mode) {
+    if (!c) return PT_E_ARG;
+    if (mode < 1 || mode > 4) return fail(c, PT_E_ARG, "display_mode must be 1..4");
+    if (mode != c->cfg.display_mode) drop_graph(c);   // a captured graph bakes in the mode
+    c->cfg.display_mode = mode;
+    return PT_OK;
+}
+
 int pt_set_counting(pt_ctx* c, int enable) {
     if (!c) return PT_E_ARG;
     // graph replays never count (pt_progressive_setup refuses counting): a graph captured

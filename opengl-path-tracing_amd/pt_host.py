@@ -9,7 +9,7 @@ Names follow the reference so that its call sequence reads the same:
     .dispatch(frame, accumulate)        one reference dispatch (uniforms frame/accumulate)
     .render(frame_first, n, acc_first)  n dispatches fused in one launch (bit-identical)
 Errors raise PTError carrying the library's code and message (the reference prints and
-continues; the drop-in fails loudly instead -- DESIGN.md §2.4).
+continues; the drop-in fails loudly instead -- DESIGN.md §1).
 
 There is no CPU fallback: if the HIP library is missing or no device is present, the
 calls raise.  The CPU oracle lives in oracle/ and is only used by tests and the bench's
@@ -44,6 +44,12 @@ class PTError(RuntimeError):
 class _Config(C.Structure):
     _fields_ = [(n, C.c_int) for n in ("width", "height", "max_bounce", "display_mode", "flags",
                                        "rays_per_pixel", "device", "rank", "world")]
+
+
+class ViewerFrame(C.Structure):
+    """pt_viewer_frame_info (include/pt_viewer.h)."""
+    _fields_ = [("camera", C.c_float * 12), ("frame", C.c_int), ("accumulate", C.c_int),
+                ("display_mode", C.c_int), ("should_close", C.c_int)]
 
 
 _lib = None
@@ -102,6 +108,15 @@ def lib():
             "pt_progressive_setup": (ip, [vp, ip, ip]),
             "pt_progressive_reset": (ip, [vp, ip]),
             "pt_progressive_run": (ip, [vp, ip]),
+            "pt_set_display_mode": (ip, [vp, ip]),
+            "pt_viewer_create": (ip, [vp, ip, C.POINTER(vp)]),
+            "pt_viewer_destroy": (None, [vp]),
+            "pt_viewer_set_params": (ip, [vp, fp, fp, ip]),
+            "pt_viewer_key": (ip, [vp, ip, ip]),
+            "pt_viewer_cursor": (ip, [vp, C.c_double, C.c_double]),
+            "pt_viewer_should_close": (ip, [vp]),
+            "pt_viewer_next": (ip, [vp, C.c_double, C.POINTER(ViewerFrame)]),
+            "pt_viewer_frame": (ip, [vp, vp, C.c_double, C.POINTER(ViewerFrame)]),
         }
         for name, (res, args) in sig.items():
             fn = getattr(L, name)
@@ -115,7 +130,7 @@ def header_symbols():
     """Function names declared in include/*.h (for the ABI export test)."""
     import re
     names = []
-    for h in ("pt_api.h", "pt_scene.h"):
+    for h in ("pt_api.h", "pt_scene.h", "pt_viewer.h"):
         txt = open(os.path.join(INCLUDE_DIR, h)).read()
         txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
         names += re.findall(r"\b(pt_[a-z0-9_]+)\s*\(", txt)
@@ -273,6 +288,10 @@ class PathTracer:
     def set_camera(self, cam):
         self._check(lib().pt_set_camera(self.h, np.ascontiguousarray(cam, np.float32).reshape(12)))
 
+    def set_display_mode(self, mode):
+        """Uniform displayMode (ogl_path_trace.h:182)."""
+        self._check(lib().pt_set_display_mode(self.h, int(mode)))
+
     def set_counting(self, on=True):
         self._check(lib().pt_set_counting(self.h, int(bool(on))))
 
@@ -373,6 +392,68 @@ class PathTracer:
         self._check(lib().pt_stats(self.h, C.byref(ms), cnt))
         return ms.value, dict(segments=int(cnt[0]), node_visits=int(cnt[1]), tri_tests=int(cnt[2]),
                               sphere_tests=int(cnt[3]), hits=int(cnt[4]))
+
+
+# ----------------------------------------------------------------------------- interactive loop
+# GLFW key codes / actions the reference's key callback tests (ogl_path_trace.h:258-299)
+KEY_SPACE, KEY_1, KEY_2, KEY_3, KEY_4 = 32, 49, 50, 51, 52
+KEY_A, KEY_D, KEY_S, KEY_W, KEY_ESCAPE, KEY_LEFT_SHIFT = 65, 68, 83, 87, 256, 340
+RELEASE, PRESS, REPEAT = 0, 1, 2
+
+
+class Viewer:
+    """The reference's render loop without its window (include/pt_viewer.h): GLFW
+    callbacks handleMovementInput / cursorPosCallback, then one frame per frame() call."""
+
+    def __init__(self, camera=None, display_mode=1, move_speed=10.0, rot_speed=0.1, accumulate=1):
+        h = C.c_void_p()
+        cam = None if camera is None else np.ascontiguousarray(camera, np.float32).reshape(12)
+        rc = lib().pt_viewer_create(None if cam is None else cam.ctypes.data, int(display_mode), C.byref(h))
+        if rc:
+            raise PTError(rc, "pt_viewer_create")
+        self.h = h
+        self._cam = cam
+        self._check(lib().pt_viewer_set_params(self.h, move_speed, rot_speed, int(accumulate)))
+
+    def _check(self, rc):
+        if rc:
+            raise PTError(rc, "pt_viewer")
+
+    def close(self):
+        if getattr(self, "h", None):
+            lib().pt_viewer_destroy(self.h)
+            self.h = None
+
+    __del__ = close
+
+    def key(self, key, action):
+        self._check(lib().pt_viewer_key(self.h, int(key), int(action)))
+
+    def cursor(self, x, y):
+        self._check(lib().pt_viewer_cursor(self.h, float(x), float(y)))
+
+    @property
+    def should_close(self):
+        return bool(lib().pt_viewer_should_close(self.h))
+
+    @staticmethod
+    def _info(fi):
+        return dict(camera=np.array(fi.camera[:], np.float32), frame=fi.frame, accumulate=fi.accumulate,
+                    display_mode=fi.display_mode, should_close=bool(fi.should_close))
+
+    def next(self, now):
+        """Host side of one loop iteration -> its dispatch parameters."""
+        fi = ViewerFrame()
+        self._check(lib().pt_viewer_next(self.h, float(now), C.byref(fi)))
+        return self._info(fi)
+
+    def frame(self, pt, now):
+        """One loop iteration rendered on PathTracer pt."""
+        fi = ViewerFrame()
+        rc = lib().pt_viewer_frame(self.h, pt.h, float(now), C.byref(fi))
+        if rc:
+            raise PTError(rc, lib().pt_last_error(pt.h).decode())
+        return self._info(fi)
 
 
 def assemble_rows(parts, height):

@@ -812,4 +812,131 @@ void oracle_aces_rgba8(const float* rgba, int n_pixels, unsigned char* out) {
     }
 }
 
+// The interactive loop of run() (ogl_path_trace.h:160-204) with its two GLFW callbacks
+// (handleMovementInput :258-299, cursorPosCallback :332-364) and updateCameraBuffer
+// (:301-328), replayed from an event list:
+//   kind[i] 0: one loop iteration at glfwGetTime() = a[i]; 1: key callback (key[i],
+//   action[i]); 2: cursor callback (a[i], b[i]).
+// The loop ends early once Escape was pressed (glfwWindowShouldClose, :160).  Per frame
+// the dispatch parameters are written: cam_out 12 floats {position, direction, 0},
+// fia_out 3 ints {frame, accumulate, displayMode}.  Returns the number of frames.
+// glm is restated from its generic (non-SIMD) code: vec4 dot = (xx + yy) + (zz + ww),
+// normalize = v * (1 / sqrt(dot)), radians(d) = d * 0.01745329251994329576923690768489.
+struct GVec4 { float x, y, z, w; };
+
+int oracle_viewer_replay(int n_events, const int* kind, const double* a, const double* b, const int* key,
+                         const int* action, const float* cam0, int display_mode0, float moveSpeed,
+                         float rotSpeed, int userDefinedAccumulate, int max_frames, float* cam_out,
+                         int* fia_out) {
+    const float PI = 3.141592f;
+    GVec4 camera_position = {0.0f, -6.0f, 1.0f, 0.0f}, camera_direction = {0.0f, 1.0f, 0.0f, 0.0f};
+    if (cam0) {
+        camera_position = {cam0[0], cam0[1], cam0[2], cam0[3]};
+        camera_direction = {cam0[4], cam0[5], cam0[6], cam0[7]};
+    }
+    bool mF = false, mB = false, mL = false, mR = false, mU = false, mD = false, mC = false;
+    bool window_should_close = false;
+    double pxpos = 0, pypos = 0;
+    int displayMode = display_mode0, accumulate = 0, frameCount = 0;
+    float deltaTime = 0.0f, lastFrameTime = 0.0f;
+    int frames = 0;
+    bool first = true;
+    for (int i = 0; i < n_events; i++) {
+        if (kind[i] == 1) {                      // handleMovementInput
+            const int k = key[i], act = action[i];
+            const int prevDisplayMode = displayMode;
+            if (k == 49) displayMode = 1;
+            if (k == 50) displayMode = 2;
+            if (k == 51) displayMode = 3;
+            if (k == 52) displayMode = 4;
+            if (prevDisplayMode != displayMode) mC = true;
+            if (k == 87) { if (act == 1) mF = true; if (act == 0) mF = false; }
+            if (k == 65) { if (act == 1) mL = true; if (act == 0) mL = false; }
+            if (k == 83) { if (act == 1) mB = true; if (act == 0) mB = false; }
+            if (k == 68) { if (act == 1) mR = true; if (act == 0) mR = false; }
+            if (k == 32) { if (act == 1) mU = true; if (act == 0) mU = false; }
+            if (k == 340) { if (act == 1) mD = true; if (act == 0) mD = false; }
+            if (k == 256) window_should_close = true;
+            continue;
+        }
+        if (kind[i] == 2) {                      // cursorPosCallback
+            const double xpos = a[i], ypos = b[i];
+            mC = true;
+            double rotationAroundZ = ((pxpos - xpos) * 0.01745329251994329576923690768489) * (double)rotSpeed;
+            double rotationAroundHoriz = ((pypos - ypos) * 0.01745329251994329576923690768489) * (double)rotSpeed;
+            float lz2 = camera_direction.x * camera_direction.x + camera_direction.y * camera_direction.y;
+            double lengthFromZPerspective = (double)sqrtf(lz2);
+            double currentZAngle = (double)atan2f(camera_direction.y, camera_direction.x);
+            double newZAngle = currentZAngle + rotationAroundZ;
+            float l2 = camera_direction.x * camera_direction.x + camera_direction.y * camera_direction.y;
+            l2 = l2 + camera_direction.z * camera_direction.z;
+            double length = (double)sqrtf(l2);
+            double currentHAngle = atan2((double)camera_direction.z, lengthFromZPerspective);
+            double newHAngle = currentHAngle + rotationAroundHoriz;
+            const double half_pi = (double)PI / 2.0, neg_half_pi = (double)(-PI) / 2.0;
+            if (newHAngle > half_pi || newHAngle < neg_half_pi) newHAngle = currentHAngle;
+            double newZ = length * sin(newHAngle);
+            double newXYLength = length * cos(newHAngle);
+            double newX = newXYLength * cos(newZAngle);
+            double newY = newXYLength * sin(newZAngle);
+            camera_direction = {(float)newX, (float)newY, (float)newZ, 0.0f};
+            pxpos = xpos;
+            pypos = ypos;
+            continue;
+        }
+        // one loop iteration
+        if (window_should_close || frames >= max_frames) break;
+        if (!first) {                            // tail of the previous iteration
+            accumulate = userDefinedAccumulate;
+            if (mF || mR || mB || mL || mU || mD || mC) {
+                accumulate = 0;
+                frameCount = 0;
+            }
+            mC = false;
+        }
+        first = false;
+        // updateCameraBuffer
+        GVec4 t = {camera_direction.x - 0.0f, camera_direction.y - 0.0f, camera_direction.z - camera_direction.z,
+                   camera_direction.w - 0.0f};
+        float dd = (t.x * t.x + t.y * t.y) + (t.z * t.z + t.w * t.w);
+        float inv = 1.0f / sqrtf(dd);
+        GVec4 forward = {t.x * inv, t.y * inv, t.z * inv, t.w * inv};
+        // cross(forward3, (0,0,1))
+        GVec4 right = {forward.y * 1.0f - 0.0f * forward.z, forward.z * 0.0f - 1.0f * forward.x,
+                       forward.x * 0.0f - 0.0f * forward.y, 0.0f};
+        GVec4 up = {0.0f, 0.0f, 1.0f, 0.0f};
+        auto step = [&](const GVec4& v, float sign) {
+            const float sx = (v.x * moveSpeed) * deltaTime, sy = (v.y * moveSpeed) * deltaTime;
+            const float sz = (v.z * moveSpeed) * deltaTime, sw = (v.w * moveSpeed) * deltaTime;
+            if (sign > 0) {
+                camera_position = {camera_position.x + sx, camera_position.y + sy, camera_position.z + sz,
+                                   camera_position.w + sw};
+            } else {
+                camera_position = {camera_position.x - sx, camera_position.y - sy, camera_position.z - sz,
+                                   camera_position.w - sw};
+            }
+        };
+        if (mF) step(forward, 1.0f);
+        if (mL) step(right, -1.0f);
+        if (mB) step(forward, -1.0f);
+        if (mR) step(right, 1.0f);
+        if (mU) step(up, 1.0f);
+        if (mD) step(up, -1.0f);
+        frameCount++;
+        float currentTime = (float)a[i];
+        deltaTime = currentTime - lastFrameTime;
+        lastFrameTime = currentTime;
+        float* c = cam_out + 12 * frames;
+        const float buf[12] = {camera_position.x, camera_position.y, camera_position.z, camera_position.w,
+                               camera_direction.x, camera_direction.y, camera_direction.z, camera_direction.w,
+                               0.0f, 0.0f, 0.0f, 0.0f};
+        std::memcpy(c, buf, sizeof(buf));
+        fia_out[3 * frames + 0] = frameCount;
+        fia_out[3 * frames + 1] = accumulate;
+        fia_out[3 * frames + 2] = displayMode;
+        frames++;
+    }
+    return frames;
+}
+
 }  // extern "C"

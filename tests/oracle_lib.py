@@ -51,6 +51,10 @@ def lib():
         L.oracle_render_pixels.argtypes = scene + [C.c_int] * 9 + [I, I, C.c_int, F, C.c_int,
                                                                    C.c_void_p]
         L.oracle_aces_rgba8.argtypes = [F, C.c_int, U8]
+        D = np.ctypeslib.ndpointer(np.float64, flags="C_CONTIGUOUS")
+        L.oracle_viewer_replay.restype = C.c_int
+        L.oracle_viewer_replay.argtypes = [C.c_int, I, D, D, I, I, C.c_void_p, C.c_int, C.c_float, C.c_float,
+                                           C.c_int, C.c_int, F, I]
         for fn in (L.oracle_mt_triangle, L.oracle_hit_triangle):
             fn.restype = C.c_float
             fn.argtypes = [F, F, F, F]
@@ -154,3 +158,30 @@ def triangle_test(o, d, tri, mt=False):
     fn = lib().oracle_mt_triangle if mt else lib().oracle_hit_triangle
     t = fn(np.asarray(o, np.float32), np.asarray(d, np.float32), np.ascontiguousarray(tri, np.float32), n)
     return np.float32(t), n
+
+
+def viewer_replay(events, camera=None, display_mode=1, move_speed=10.0, rot_speed=0.1, accumulate=1):
+    """Restated interactive loop (ogl_path_trace.h:160-204, 258-364) over an event list of
+    ("frame", t) / ("key", code, action) / ("cursor", x, y) -> list of per-frame dicts
+    {camera[12], frame, accumulate, display_mode}."""
+    n = len(events)
+    kind = np.zeros(max(n, 1), np.int32)
+    a = np.zeros(max(n, 1), np.float64)
+    b = np.zeros(max(n, 1), np.float64)
+    key = np.zeros(max(n, 1), np.int32)
+    act = np.zeros(max(n, 1), np.int32)
+    for i, e in enumerate(events):
+        if e[0] == "frame":
+            a[i] = e[1]
+        elif e[0] == "key":
+            kind[i], key[i], act[i] = 1, e[1], e[2]
+        else:
+            kind[i], a[i], b[i] = 2, e[1], e[2]
+    nf = max(1, sum(1 for e in events if e[0] == "frame"))
+    cam_out = np.zeros(12 * nf, np.float32)
+    fia = np.zeros(3 * nf, np.int32)
+    cam = None if camera is None else np.ascontiguousarray(camera, np.float32).reshape(12)
+    got = lib().oracle_viewer_replay(n, kind, a, b, key, act, None if cam is None else cam.ctypes.data,
+                                     display_mode, move_speed, rot_speed, accumulate, nf, cam_out, fia)
+    return [dict(camera=cam_out[12 * i: 12 * i + 12].copy(), frame=int(fia[3 * i]), accumulate=int(fia[3 * i + 1]),
+                 display_mode=int(fia[3 * i + 2])) for i in range(got)]
