@@ -37,7 +37,43 @@ static void usage() {
                  "              key K ACTION       key callback; K = GLFW code or w a s d 1-4 space shift esc,\n"
                  "                                 ACTION = press | release | repeat\n"
                  "              cursor X Y         cursor callback\n"
-                 "            '#' starts a comment; the loop ends early once esc was pressed\n");
+                 "            '#' starts a comment; the loop ends early once esc was pressed\n"
+                 "  --checkpoint F  after rendering, save the RGBA32F accumulation and the next frame\n"
+                 "                  number (text header 'PTCK1 W H next_frame', then W*H*4 floats)\n"
+                 "  --resume F      continue a saved accumulation: frames next_frame.. with accumulate = 1,\n"
+                 "                  the same image as one uninterrupted run\n"
+                 "  --json          print a JSON summary line\n");
+}
+
+// Checkpoint of a progressive render (SURVEY.md §5 checkpoint / resume): the running mean
+// (computeShader.c:548-551) only needs the accumulation image and the next frame number.
+static bool save_checkpoint(const std::string& path, int W, int H, int next_frame, const std::vector<float>& img) {
+    FILE* f = std::fopen(path.c_str(), "wb");
+    if (!f) return false;
+    std::fprintf(f, "PTCK1 %d %d %d\n", W, H, next_frame);
+    const bool ok = std::fwrite(img.data(), 4, img.size(), f) == img.size();
+    return std::fclose(f) == 0 && ok;
+}
+
+static bool load_checkpoint(const std::string& path, int W, int H, int& next_frame, std::vector<float>& img,
+                            std::string& err) {
+    FILE* f = std::fopen(path.c_str(), "rb");
+    if (!f) { err = "cannot open " + path; return false; }
+    int w = 0, h = 0, nf = 0;
+    char magic[8] = {0};
+    bool ok = std::fscanf(f, "%5s %d %d %d", magic, &w, &h, &nf) == 4 && std::string(magic) == "PTCK1" &&
+              std::fgetc(f) == '\n';
+    if (!ok) err = path + ": not a PTCK1 checkpoint";
+    else if (w != W || h != H) { ok = false; err = path + ": checkpoint is " + std::to_string(w) + "x" + std::to_string(h); }
+    else if (nf < 1) { ok = false; err = path + ": bad next frame"; }
+    if (ok) {
+        img.assign(4 * (size_t)W * H, 0.0f);
+        ok = std::fread(img.data(), 4, img.size(), f) == img.size();
+        if (!ok) err = path + ": truncated";
+        next_frame = nf;
+    }
+    std::fclose(f);
+    return ok;
 }
 
 // One event of an --events script (see usage()).
@@ -115,8 +151,9 @@ int main(int argc, char** argv) {
     int W = 1000, H = 800, spp = 64, chunk = 16, bounces = 5, mode = 1, gpus = 1;   // ogl_path_trace.h:45-46
     std::string pfm = "out.pfm", ppm = "out.ppm";
     float cam[12] = {0, -6, 1, 0, 0, 1, 0, 0, 0, 0, 0, 0};                          // ogl_path_trace.h:53-54
-    bool robust = false;
+    bool robust = false, json = false;
     const char* events = nullptr;
+    std::string checkpoint, resume;
     for (int i = 3; i < argc; i++) {
         std::string a = argv[i];
         auto next = [&](void) -> const char* { if (i + 1 >= argc) { usage(); std::exit(2); } return argv[++i]; };
@@ -132,9 +169,22 @@ int main(int argc, char** argv) {
         else if (a == "--camera") { for (int k = 0; k < 6; k++) cam[k < 3 ? k : k + 1] = (float)std::atof(next()); }
         else if (a == "--robust") robust = true;
         else if (a == "--events") events = next();
+        else if (a == "--checkpoint") checkpoint = next();
+        else if (a == "--resume") resume = next();
+        else if (a == "--json") json = true;
         else { usage(); return 2; }
     }
     if (spp < 1 || chunk < 1 || gpus < 1) { usage(); return 2; }
+    if (events && (!resume.empty() || !checkpoint.empty())) {
+        std::fprintf(stderr, "--events excludes --resume / --checkpoint\n");
+        return 2;
+    }
+    int first = 1;                        // frame number of the first frame rendered
+    std::vector<float> prior;
+    if (!resume.empty()) {
+        std::string err;
+        if (!load_checkpoint(resume, W, H, first, prior, err)) { std::fprintf(stderr, "%s\n", err.c_str()); return 2; }
+    }
 
     auto t0 = std::chrono::steady_clock::now();
     pt_scene* sc = nullptr;
@@ -162,6 +212,14 @@ int main(int argc, char** argv) {
         CHECK(pt_create(&cfg, &ctx[g]), ctx[g]);
         CHECK(pt_upload_scene(ctx[g], tris.data(), cnt[0], nodes.data(), cnt[3], mats.data(), cnt[1], sph.data(), cnt[2]), ctx[g]);
         CHECK(pt_set_camera(ctx[g], cam), ctx[g]);
+        if (!prior.empty()) {             // this context's rows of the saved image
+            int rows = 0, r0 = 0, rs = 1;
+            pt_rows(ctx[g], &rows, &r0, &rs);
+            std::vector<float> part(4 * (size_t)rows * W);
+            for (int k = 0; k < rows; k++)
+                std::memcpy(&part[4 * (size_t)k * W], &prior[4 * (size_t)(r0 + k * rs) * W], 16 * (size_t)W);
+            CHECK(pt_write_rgba32f(ctx[g], part.data(), part.size() * 4), ctx[g]);
+        }
     }
     auto t1 = std::chrono::steady_clock::now();
     int frames_run = 0, resets = 0;
@@ -191,8 +249,9 @@ int main(int argc, char** argv) {
         pt_viewer_destroy(view);
         spp = frames_run;
     } else {
-        for (int f0 = 1; f0 <= spp; f0 += chunk) {
-            int n = std::min(chunk, spp - f0 + 1);
+        for (int k = 0; k < spp; k += chunk) {
+            const int n = std::min(chunk, spp - k), f0 = first + k;
+            // frame 1 after a reset overwrites (accumulate = 0); a resumed run accumulates
             for (int g = 0; g < gpus; g++) CHECK(pt_render_async(ctx[g], f0, n, f0 == 1 ? 0 : 1), ctx[g]);
         }
     }
@@ -218,6 +277,16 @@ int main(int argc, char** argv) {
     }
     std::printf("rendered %dx%d, %d spp, %d bounces on %d GPU(s): %.3f s, %.3f ms/frame\n", W, H, spp, bounces,
                 gpus, secs, secs * 1e3 / (spp > 0 ? spp : 1));
+    if (!checkpoint.empty()) {
+        if (!save_checkpoint(checkpoint, W, H, first + spp, img)) {
+            std::fprintf(stderr, "cannot write checkpoint %s\n", checkpoint.c_str());
+            return 1;
+        }
+    }
+    if (json)
+        std::printf("{\"width\": %d, \"height\": %d, \"frames\": %d, \"first_frame\": %d, \"bounces\": %d, "
+                    "\"gpus\": %d, \"seconds\": %.6f, \"ms_per_frame\": %.4f, \"triangles\": %d, \"nodes\": %d}\n",
+                    W, H, spp, first, bounces, gpus, secs, secs * 1e3 / (spp > 0 ? spp : 1), cnt[0], cnt[3]);
 
     if (FILE* f = std::fopen(pfm.c_str(), "wb")) {       // PFM rows run bottom-to-top: no flip
         std::fprintf(f, "PF\n%d %d\n-1.0\n", W, H);

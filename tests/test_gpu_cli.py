@@ -48,3 +48,40 @@ def test_cli_matches_oracle(tmp_path, chunk):
     assert np.array_equal(got.view(np.uint32), np.ascontiguousarray(want[..., :3]).view(np.uint32))
     # the PPM is the ACES view, rows top to bottom
     assert np.array_equal(read_ppm(ppm), O.aces_rgba8(want)[::-1, :, :3])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("gpus", [1])
+def test_cli_checkpoint_resume_is_one_run(tmp_path, gpus):
+    """--checkpoint / --resume: 4 frames, saved, then 3 more resumed, equal
+    bit for bit to one 7-frame run and to the oracle."""
+    obj, mtl = pt_scenes.write_scene("cornell", str(tmp_path))
+    W, Hh = 40, 30
+    common = [EXE, obj, mtl, "--width", str(W), "--height", str(Hh), "--bounces", "8", "--chunk", "2",
+              "--gpus", str(gpus), "--ppm", str(tmp_path / "x.ppm")]
+    ck = str(tmp_path / "run.ptck")
+    a = subprocess.run(common + ["--spp", "4", "--checkpoint", ck, "--pfm", str(tmp_path / "a.pfm")],
+                       capture_output=True, text=True, timeout=120)
+    assert a.returncode == 0, a.stderr
+    with open(ck, "rb") as f:
+        assert f.readline().split() == [b"PTCK1", str(W).encode(), str(Hh).encode(), b"5"]
+    b = subprocess.run(common + ["--spp", "3", "--resume", ck, "--pfm", str(tmp_path / "b.pfm"), "--json"],
+                       capture_output=True, text=True, timeout=120)
+    assert b.returncode == 0, b.stderr
+    import json
+    summary = json.loads(b.stdout.strip().splitlines()[-1])
+    assert summary["first_frame"] == 5 and summary["frames"] == 3
+    want = O.render(H.setupBuffers(obj, mtl), W, Hh, max_bounce=8, n_frames=7)
+    got = read_pfm(str(tmp_path / "b.pfm"))
+    assert np.array_equal(got.view(np.uint32), np.ascontiguousarray(want[..., :3]).view(np.uint32))
+
+
+def test_cli_rejects_bad_checkpoint(tmp_path, cornell_paths):
+    bad = tmp_path / "bad.ptck"
+    bad.write_bytes(b"PTCK1 8 8 3\n" + b"\0" * 16)
+    out = subprocess.run([EXE, *cornell_paths, "--width", "8", "--height", "8", "--resume", str(bad)],
+                         capture_output=True, text=True, timeout=60)
+    assert out.returncode == 2 and "truncated" in out.stderr
+    out = subprocess.run([EXE, *cornell_paths, "--width", "9", "--height", "8", "--resume", str(bad)],
+                         capture_output=True, text=True, timeout=60)
+    assert out.returncode == 2 and "checkpoint is 8x8" in out.stderr
