@@ -2615,6 +2615,20 @@ static int plan_group(const pt_ctx* c, int n_frames) {
     return std::min(g, n_frames);
 }
 
+// Whether a launch of n_frames with frames-per-item `group` runs in frame-split mode
+// (colour planes + k_accum_frames).  Register mode (group == n_frames: a lane owns whole
+// pixels, the running mean in registers) pulls one queue id per lane without batching, which
+// is right for long items.  But a launch of a few frames has items of a few segments, and
+// the chip-wide queue counter then throttles the kernel: one 1080p frame per launch (the
+// reference's one dispatch per displayed frame) took 3.2 ms of kernel time, against 0.5 ms
+// per frame in long launches.  In automatic mode such launches use the split path and its
+// batched reservations; pt_set_tuning key 5 >= n_frames still forces register mode.
+constexpr int kShortLaunch = 16;
+static bool split_mode(const pt_ctx* c, int n_frames, int group) {
+    if (group < n_frames) return true;
+    return c->group_force == 0 && (c->variant == 0 || c->variant == 3) && n_frames <= kShortLaunch;
+}
+
 // Grows the frame-split scratch to n_frames frame planes.  Earlier launches on the stream may
 // still read the old buffer, so the stream is drained first; a buffer a captured graph was
 // built with is handed to the graph (freed by drop_graph) instead of being freed under it.
@@ -2672,7 +2686,7 @@ static int launch_frames(const pt_ctx* c, int n_frames) {
     int n = n_frames;
     for (;;) {
         const int g = plan_group(c, n);
-        if (g >= n && !wf_paths(c, n)) return n;    // register mode: no scratch, one group
+        if (!split_mode(c, n, g) && !wf_paths(c, n)) return n;    // register mode: no scratch, one group
         const unsigned long long by_budget = c->scratch_budget / (px * 12ull);
         const unsigned long long ng = (unsigned long long)((n + g - 1) / g);
         const unsigned long long by_ids = (kIdLimit / tiles64) * (unsigned long long)g;
@@ -2741,7 +2755,7 @@ static int enqueue_render(pt_ctx* c, int frame_first, int n_frames, int acc_firs
         p.grp_magic = (ng > 1 && items * ng < (1ull << 32)) ? (unsigned)(((1ull << 32) + ng - 1) / ng) : 0u;
     }
     const int wfP = wf_paths(c, n_frames);
-    if (p.group < n_frames || wfP) {
+    if (split_mode(c, n_frames, p.group) || wfP) {
         int rc = ensure_rgb(c, n_frames);
         if (rc) return rc;
         p.rgb = c->d_rgb;
@@ -2916,7 +2930,7 @@ int pt_progressive_setup(pt_ctx* c, int frames_per_launch, int launches_per_repl
     if (!c->d_frame) HIPCHK(c, hipMalloc(&c->d_frame, 64));
     {   // no allocation inside the capture: the scratch of the largest sub-launch first
         const int n = launch_frames(c, frames_per_launch);
-        if (plan_group(c, n) < n) {
+        if (split_mode(c, n, plan_group(c, n))) {
             int rc0 = ensure_rgb(c, n);
             if (rc0) return rc0;
         }

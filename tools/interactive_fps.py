@@ -1,0 +1,62 @@
+"""Interactive-loop rate with the image crossing PCIe every frame: the
+reference's render loop (one dispatch per displayed frame, ogl_path_trace.h:160-204) through
+pt_viewer_frame, each frame followed by the readback a window would upload -- the ACES RGBA8
+view (pt_read_rgba8_aces) or the raw RGBA32F accumulation.  Scene and accumulator stay in HBM;
+only the frame crosses to the host.  One GPU.
+
+python tools/interactive_fps.py [--width 1920 --height 1080 --frames 300]
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(REPO, "opengl-path-tracing_amd"))
+import pt_host as H  # noqa: E402
+import pt_scenes  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--width", type=int, default=1920)
+    ap.add_argument("--height", type=int, default=1080)
+    ap.add_argument("--frames", type=int, default=300)
+    ap.add_argument("--bounces", type=int, default=8)
+    ap.add_argument("--scene", default="cornell")
+    a = ap.parse_args()
+    sb = H.setupBuffers(*pt_scenes.write_scene(a.scene, os.path.join(REPO, "scenes")))
+    pt = H.PathTracer(a.width, a.height, max_bounce=a.bounces)
+    t0 = time.perf_counter()
+    pt.upload(sb)
+    upload_s = time.perf_counter() - t0
+    # segments per frame from an untimed counting pass over frames 1..8
+    pt.set_counting(True)
+    pt.render(1, 8, 0)
+    seg_per_frame = pt.stats()[1]["segments"] / 8.0
+    pt.set_counting(False)
+    out = {"width": a.width, "height": a.height, "bounces": a.bounces, "scene": a.scene, "frames": a.frames,
+           "scene_upload_ms": round(upload_s * 1e3, 3), "segments_per_frame": seg_per_frame}
+    for readback in ("none", "rgba8_aces", "rgba32f"):
+        v = H.Viewer()
+        for i in range(10):                                   # warm-up
+            v.frame(pt, 0.001 * i)
+            pt.read_rgba8()
+        t0 = time.perf_counter()
+        for i in range(a.frames):
+            v.frame(pt, 1.0 + 0.001 * i)                      # pt_render is synchronous
+            if readback == "rgba8_aces":
+                pt.read_rgba8()
+            elif readback == "rgba32f":
+                pt.read_rgba32f()
+        dt = time.perf_counter() - t0
+        v.close()
+        out[readback] = {"ms_per_frame": round(dt * 1e3 / a.frames, 4), "fps": round(a.frames / dt, 1),
+                         "mrays_per_s": round(seg_per_frame * a.frames / dt / 1e6, 1)}
+    pt.close()
+    print(json.dumps(out))
+
+
+if __name__ == "__main__":
+    main()
