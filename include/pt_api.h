@@ -136,9 +136,13 @@ int pt_set_kernel(pt_ctx* ctx, int variant);
  *         the segment counts of the previous renders; 0 = raster order),
  * key 3 = resident waves per SIMD the kernel is compiled for (5..8; 0 = auto: 7 for scenes
  *         staged in LDS, 6 for global-memory scenes),
+ * key 4 = queue ids a wave reserves per queue atomic in frame-split mode (32..1024; 0 = auto:
+ *         128 / 64 for LDS-staged scenes with items of 1 / 2 frames, else 32).
  * key 5 = frames per work item (>= 1; 0 = auto, 2..8): a pixel's frames are spread over
  *         several lanes and the running mean is applied by a second kernel in frame order;
  *         a value >= n_frames gives each lane whole pixels (running mean in registers).
+ *         In automatic mode launches of at most 16 frames always take the split path (its
+ *         batched queue reservations), whatever their group.
  * key 6 = walk floor (1..64, 0 = auto): a walk phase ends once fewer lanes than this still
  *         walk, and the leaf (or shading) phase runs even below its threshold.
  * key 7 = leaf-phase compaction limit (0..63, default 63): the edge tests of a wave's leaf

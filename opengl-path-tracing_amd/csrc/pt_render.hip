@@ -63,6 +63,7 @@ struct KParams {
     int leaf_thresh, shade_thresh; // wave scheduling thresholds of the state-machine kernel
     int trav_floor;                // ... and the walk floor: fewer walking lanes end a walk phase
     int compact_max;               // leaf phase: compact the edge tests of at most this many pairs (<= 63)
+    int pull_batch;                // frame-split mode: queue ids a wave reserves per queue atomic (>= 32)
     const int* frame_dev;          // progressive graph: device frame counter (null = use frame_first)
     int frame_offset;              // this launch's frame offset from *frame_dev
     const unsigned* tile_perm;     // queue order of 8x8 tiles, entries (ty << 16) | tx (null = raster order)
@@ -1297,7 +1298,7 @@ __global__ __launch_bounds__(256, MINW) void k_render_sm(KParams p) {
                     qnext += need;
                 } else {
                     const unsigned avail = SPLIT ? qend - qnext : 0u;
-                    const unsigned take = SPLIT ? max(need - avail, kPullBatch) : need;
+                    const unsigned take = SPLIT ? max(need - avail, (unsigned)p.pull_batch) : need;
                     unsigned base = 0;
                     if (want && rank == 0u) base = atomicAdd(p.work_counter, take);   // the leader
                     base = (unsigned)__builtin_amdgcn_readlane((int)base, leader);
@@ -1476,6 +1477,46 @@ __global__ __launch_bounds__(256, MINW) void k_render_sm(KParams p) {
     }
 #endif
     flush_counters<COUNT>(p, c);
+}
+
+// Adaptive tile order, on the device after every launch that recorded tile
+// costs: longest-processing-time-first order of the 8x8 tiles for the next launches -- a
+// counting sort of the recorded segment counts into 1024 buckets, most expensive first --
+// then the counts are cleared.  Stream-ordered, so the next launch reads the new order with
+// no host round trip (the host form cost ~0.2 ms per pt_render: three synchronous copies).
+// The order inside a bucket is whatever the LDS atomics give: tile order changes only the
+// launch tail, never the image.  One 1024-thread workgroup.
+__global__ __launch_bounds__(1024) void k_tile_order(unsigned* __restrict__ cost, unsigned* __restrict__ perm,
+                                                     int n_tiles, int tiles_x) {
+    constexpr int nb = 1024;
+    __shared__ unsigned hist[nb], base[nb], wmax[16];
+    const int tid = threadIdx.x;
+    unsigned mx = 1u;
+    for (int t = tid; t < n_tiles; t += 1024) mx = max(mx, cost[t]);
+    for (int o = 32; o > 0; o >>= 1) mx = max(mx, (unsigned)__shfl_xor((int)mx, o));
+    if ((tid & 63) == 0) wmax[tid >> 6] = mx;
+    hist[tid] = 0u;
+    __syncthreads();
+    mx = wmax[0];
+    for (int w = 1; w < 16; w++) mx = max(mx, wmax[w]);
+    auto bucket = [&](unsigned v) { return nb - 1 - (int)((unsigned long long)v * (nb - 1) / mx); };
+    for (int t = tid; t < n_tiles; t += 1024) atomicAdd(&hist[bucket(cost[t])], 1u);
+    __syncthreads();
+    const unsigned own = hist[tid];
+    for (int off = 1; off < nb; off <<= 1) {      // inclusive scan of the bucket sizes
+        const unsigned add = tid >= off ? hist[tid - off] : 0u;
+        __syncthreads();
+        hist[tid] += add;
+        __syncthreads();
+    }
+    base[tid] = hist[tid] - own;
+    __syncthreads();
+    for (int t = tid; t < n_tiles; t += 1024) {
+        const unsigned pos = atomicAdd(&base[bucket(cost[t])], 1u);
+        perm[pos] = ((unsigned)(t / tiles_x) << 16) | (unsigned)(t % tiles_x);
+    }
+    __syncthreads();
+    for (int t = tid; t < n_tiles; t += 1024) cost[t] = 0u;
 }
 
 // Running mean of the frame-split mode (:548-551): per local pixel, the launch's frames in
@@ -2130,7 +2171,7 @@ struct pt_ctx {
     unsigned* d_tile_cost = nullptr;
     unsigned* d_tile_perm = nullptr;
     int n_tiles = 0, tiles_x = 1;
-    bool adaptive = true, cost_pending = false;
+    bool adaptive = true;
     hipGraph_t graph = nullptr;
     hipGraphExec_t graph_exec = nullptr;
     int graph_frames = 0;
@@ -2143,7 +2184,7 @@ struct pt_ctx {
     // 16/24 when the walk reads global memory (re-swept after the leaf compaction: +2% on
     // the C3 stand-in, +3% on C4 over 16/32); walk floor 8 / 6
     // (+0.8% on C2, +0.5% on C3 over no floor) -- tools/probe.py sweeps
-    int leaf_thresh = 0, shade_thresh = 0, minw = 0, trav_floor = 0, compact_max = 63;
+    int leaf_thresh = 0, shade_thresh = 0, minw = 0, trav_floor = 0, compact_max = 63, pull_batch = 0;
     // frame-split work items (KParams::group): 0 = automatic, n = frames per item
     int group_force = 0;
     // variant 4 knobs (0 = automatic): path slots per workgroup, refill walker count,
@@ -2563,6 +2604,12 @@ int pt_set_tuning(pt_ctx* c, int key, int value) {
         drop_graph(c);
         return PT_OK;
     }
+    if (key == 4) {
+        if (value != 0 && (value < 32 || value > 1024)) return fail(c, PT_E_ARG, "pull batch must be 32..1024 (0 = auto)");
+        c->pull_batch = value;
+        drop_graph(c);
+        return PT_OK;
+    }
     if (key == 7) {
         if (value < 0 || value > 63) return fail(c, PT_E_ARG, "compaction limit must be in 0..63");
         c->compact_max = value;
@@ -2585,7 +2632,6 @@ int pt_set_tuning(pt_ctx* c, int key, int value) {
             HIPCHK(c, hipSetDevice(c->cfg.device));
             HIPCHK(c, hipStreamSynchronize(c->stream));
             HIPCHK(c, hipMemcpy(c->d_tile_perm, ident.data(), ident.size() * sizeof(unsigned), hipMemcpyHostToDevice));
-            c->cost_pending = false;
         }
     }
     else return fail(c, PT_E_ARG, "unknown tuning key");
@@ -2748,6 +2794,18 @@ static int enqueue_render(pt_ctx* c, int frame_first, int n_frames, int acc_firs
     p.fH = (float)p.H;
     p.rH = 1.0f / (float)p.H;
     p.group = plan_group(c, n_frames);
+    // queue ids reserved per queue atomic: on an LDS-staged scene an item of one or two
+    // frames is a few short segments, and the chip-wide counter then limits the launch (one
+    // 1080p Cornell frame per launch: 1.14 ms kernel time with 32 ids per reservation, 0.97
+    // with 128; 4K 3.44 -> 2.64 ms; 4-frame launches 0.83 -> 0.62 ms per frame).  A wave
+    // that reserves more ids than it soon needs lengthens the launch tail instead, so longer
+    // items and the global-memory scenes' long segments keep 32 (C3 stand-in, one frame per
+    // launch: 3.19 ms with 32, 3.63 with 128).  Tuning key 4 overrides.
+    {
+        const bool lds_items = c->lds_bytes <= kLdsSceneMax && c->variant != 3;
+        p.pull_batch = c->pull_batch ? c->pull_batch
+                                     : (lds_items && p.group <= 2 ? (p.group == 1 ? 128 : 64) : (int)kPullBatch);
+    }
     {   // exact item / n_groups by ceil(2^32 / n_groups) when item * n_groups < 2^32 for every
         // item (then floor(item * m / 2^32) = floor(item / n_groups)), else the division
         const unsigned long long ng = (unsigned long long)((n_frames + p.group - 1) / p.group);
@@ -2762,7 +2820,6 @@ static int enqueue_render(pt_ctx* c, int frame_first, int n_frames, int acc_firs
     }
     p.tile_perm = c->d_tile_perm;
     p.tile_cost = (c->adaptive && !c->counting) ? c->d_tile_cost : nullptr;
-    if (p.tile_cost) c->cost_pending = true;
     if (c->rows_local == 0) return PT_OK;
     // variants: 0 state-machine persistent (default), 1 one-lane-per-pixel tiles,
     // 2 while-while persistent, 3 = 0 with the scene forced to stay in global memory
@@ -2856,6 +2913,9 @@ static int enqueue_render(pt_ctx* c, int frame_first, int n_frames, int acc_firs
             hipLaunchKernelGGL(k_accum_frames, dim3((unsigned)((px + 255) / 256)), dim3(256), 0, c->stream, p);
         }
     }
+    if (p.tile_cost && c->n_tiles > 1)
+        hipLaunchKernelGGL(k_tile_order, dim3(1), dim3(1024), 0, c->stream, c->d_tile_cost, c->d_tile_perm,
+                           c->n_tiles, c->tiles_x);
     HIPCHK(c, hipGetLastError());
     return PT_OK;
 }
@@ -2981,7 +3041,6 @@ int pt_progressive_run(pt_ctx* c, int replays) {
     c->ev_pending.emplace_back(ev[0], ev[1]);
     HIPCHK(c, hipEventRecord(ev[0], c->stream));
     for (int r = 0; r < replays; r++) HIPCHK(c, hipGraphLaunch(c->graph_exec, c->stream));
-    if (c->adaptive && (c->variant == 0 || c->variant == 3 || c->variant == 4)) c->cost_pending = true;
     if (c->variant == 4) c->wf_check = true;
     HIPCHK(c, hipEventRecord(ev[1], c->stream));
     return PT_OK;
@@ -3010,23 +3069,6 @@ int pt_sync(pt_ctx* c) {
     if (c->count_pending) {
         HIPCHK(c, hipMemcpy(c->last_counts, c->d_counters, 16 * sizeof(unsigned long long), hipMemcpyDeviceToHost));
         c->count_pending = false;
-    }
-    if (c->cost_pending && c->n_tiles > 1) {
-        // longest-processing-time-first order of the 8x8 tiles for the next renders: a
-        // bucket sort on the measured segment counts, raster order inside a bucket
-        std::vector<unsigned> cost(c->n_tiles), perm(c->n_tiles);
-        HIPCHK(c, hipMemcpy(cost.data(), c->d_tile_cost, c->n_tiles * sizeof(unsigned), hipMemcpyDeviceToHost));
-        unsigned mx = 1;
-        for (unsigned v : cost) mx = std::max(mx, v);
-        const int nb = 1024;
-        std::vector<int> cnt(nb + 1, 0);
-        auto bucket = [&](unsigned v) { return nb - 1 - (int)((unsigned long long)v * (nb - 1) / mx); };
-        for (unsigned v : cost) cnt[bucket(v) + 1]++;
-        for (int b = 0; b < nb; b++) cnt[b + 1] += cnt[b];
-        for (int t = 0; t < c->n_tiles; t++) perm[cnt[bucket(cost[t])]++] = pack_tile(c, (unsigned)t);
-        HIPCHK(c, hipMemcpy(c->d_tile_perm, perm.data(), c->n_tiles * sizeof(unsigned), hipMemcpyHostToDevice));
-        HIPCHK(c, hipMemset(c->d_tile_cost, 0, c->n_tiles * sizeof(unsigned)));
-        c->cost_pending = false;
     }
     return PT_OK;
 }

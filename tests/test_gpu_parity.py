@@ -310,6 +310,25 @@ def test_frame_split_work_items(cornell_scene, group, rpp, variant):
     assert_bitwise(got, want, "group %d rpp %d variant %d" % (group, rpp, variant))
 
 
+@pytest.mark.parametrize("batch", [32, 128, 1024])
+def test_queue_reservation_sizes_bitwise(cornell_scene, batch):
+    """Queue ids reserved per atomic (tuning key 4) change only which lane renders what: one
+    frame per launch (the interactive loop's shape) and a 3-frame launch, on a prior image."""
+    W, Hh = 72, 40
+    rng = np.random.default_rng(3)
+    prior = rng.random((Hh, W, 4), dtype=np.float32)
+    want = O.render(cornell_scene, W, Hh, max_bounce=8, frame_first=5, n_frames=4, acc_first=1, accum=prior.copy())
+    pt = H.PathTracer(W, Hh, max_bounce=8)
+    pt.upload(cornell_scene)
+    pt.set_key(4, batch)
+    pt.write_rgba32f(prior)
+    pt.render(5, 1, 1)
+    pt.render(6, 3, 1)
+    got = pt.read_rgba32f()
+    pt.close()
+    assert_bitwise(got, want, "pull batch %d" % batch)
+
+
 def test_frame_split_footprint_and_graph(cornell_scene):
     """Frame-split mode with the REF_DISPATCH footprint (k_accum_frames must not touch
     pixels outside it) and inside a captured progressive graph."""
