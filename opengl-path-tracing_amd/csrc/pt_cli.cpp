@@ -103,7 +103,7 @@ static bool parse_events(const char* path, std::vector<Event>& ev, std::string& 
         } else if (op == "frames") {
             long n = 0;
             double t0 = 0, dt = 0;
-            ok = static_cast<bool>(ss >> n >> t0 >> dt) && n >= 0;
+            ok = static_cast<bool>(ss >> n >> t0 >> dt) && n >= 0 && n <= 10000000;
             for (long i = 0; ok && i < n; i++) { e.a = t0 + (double)i * dt; ev.push_back(e); }
         } else if (op == "key") {
             std::string k, a;
