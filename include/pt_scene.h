@@ -69,6 +69,17 @@ void pt_scene_free(pt_scene* s);
 /* Stand-alone builder on raw arrays: nodes_out needs capacity >= 2*n_tris-1 nodes. */
 int pt_bvh_build(const float* tris, int n_tris, float* nodes_out, int max_nodes, int* n_nodes);
 
+/* The same builder on GPU `device`: one tree level at a time, the
+ * chained stable centroid sorts as segmented device sorts, the prefix / suffix candidate
+ * boxes as segmented scans, the split choice one thread per node.  Output identical to
+ * pt_bvh_build (same node numbering, bounds, leaf indices and links).  Needs a GPU. */
+int pt_bvh_build_gpu(const float* tris, int n_tris, float* nodes_out, int max_nodes, int* n_nodes,
+                     int device);
+/* pt_scene_build_bvh with the GPU builder. */
+int pt_scene_build_bvh_gpu(pt_scene* s, int device);
+/* Message of the calling thread's last pt_bvh_build / pt_bvh_build_gpu failure. */
+const char* pt_bvh_last_error(void);
+
 /* ACES film tonemap (screenQuadFrag.c:12-33) of an RGBA32F image to RGBA8 on the host;
  * the device form is pt_read_rgba8_aces() in pt_api.h. */
 void pt_aces_rgba8_host(const float* rgba, long long n_pixels, unsigned char* out);

@@ -42,7 +42,8 @@ static void usage() {
                  "                  number (text header 'PTCK1 W H next_frame', then W*H*4 floats)\n"
                  "  --resume F      continue a saved accumulation: frames next_frame.. with accumulate = 1,\n"
                  "                  the same image as one uninterrupted run\n"
-                 "  --json          print a JSON summary line\n");
+                 "  --json          print a JSON summary line\n"
+                 "  --gpu-bvh       build the BVH on GPU 0 (pt_bvh_build_gpu; the same nodes)\n");
 }
 
 // Checkpoint of a progressive render (SURVEY.md §5 checkpoint / resume): the running mean
@@ -151,7 +152,7 @@ int main(int argc, char** argv) {
     int W = 1000, H = 800, spp = 64, chunk = 16, bounces = 5, mode = 1, gpus = 1;   // ogl_path_trace.h:45-46
     std::string pfm = "out.pfm", ppm = "out.ppm";
     float cam[12] = {0, -6, 1, 0, 0, 1, 0, 0, 0, 0, 0, 0};                          // ogl_path_trace.h:53-54
-    bool robust = false, json = false;
+    bool robust = false, json = false, gpu_bvh = false;
     const char* events = nullptr;
     std::string checkpoint, resume;
     for (int i = 3; i < argc; i++) {
@@ -172,6 +173,7 @@ int main(int argc, char** argv) {
         else if (a == "--checkpoint") checkpoint = next();
         else if (a == "--resume") resume = next();
         else if (a == "--json") json = true;
+        else if (a == "--gpu-bvh") gpu_bvh = true;
         else { usage(); return 2; }
     }
     if (spp < 1 || chunk < 1 || gpus < 1) { usage(); return 2; }
@@ -192,7 +194,7 @@ int main(int argc, char** argv) {
     if (mtl_from_obj && !robust) { std::fprintf(stderr, "'-' as the MTL needs --robust\n"); return 2; }
     int rc = pt_scene_load_obj_ex(obj, mtl_from_obj ? nullptr : mtl, robust ? PT_LOAD_ROBUST : PT_LOAD_REFERENCE, &sc);
     if (!rc) rc = pt_scene_add_builtins(sc);
-    if (!rc) rc = pt_scene_build_bvh(sc);
+    if (!rc) rc = gpu_bvh ? pt_scene_build_bvh_gpu(sc, 0) : pt_scene_build_bvh(sc);
     if (rc) { std::fprintf(stderr, "scene: %s (%d)\n", pt_scene_last_error(sc), rc); pt_scene_free(sc); return 1; }
     int cnt[5];
     pt_scene_counts(sc, cnt);

@@ -468,6 +468,34 @@ struct TriKeyHash {
     }
 };
 
+}  // namespace
+
+namespace pt_internal {
+
+// Index of the first triangle equal to each one (all 16 floats, operator== of triangle.h:17-20:
+// -0 == +0): the leaf index buildSAHTreeHelper finds with std::find (bvh.h:231-232), by a
+// first-occurrence hash map instead of a linear search per leaf.
+int first_equal_indices(const float* T, int n, std::vector<int>& out, std::string& err) {
+    std::unordered_map<TriKey, int, TriKeyHash> first;
+    first.reserve((size_t)n * 2);
+    out.resize(n);
+    for (int i = 0; i < n; i++) {
+        const float* t = T + 16 * (size_t)i;
+        TriKey key;
+        for (int q = 0; q < 16; q++) {
+            if (!std::isfinite(t[q])) { err = "non-finite triangle data"; return PT_E_SCENE; }
+            float v = t[q] == 0.0f ? 0.0f : t[q];   // -0 == +0 for operator==
+            std::memcpy(&key.w[q], &v, 4);
+        }
+        out[i] = first.emplace(key, i).first->second;
+    }
+    return PT_OK;
+}
+
+}  // namespace pt_internal
+
+namespace {
+
 struct Builder {
     const float* T;
     int n;
@@ -522,18 +550,10 @@ struct Builder {
     int run(float* out, int max_nodes, int* n_nodes, std::string& err) {
         tbox.resize(n);
         for (int a = 0; a < 3; a++) cen[a].resize(n);
-        std::unordered_map<TriKey, int, TriKeyHash> first;
-        first.reserve((size_t)n * 2);
-        first_equal.resize(n);
+        int rc = pt_internal::first_equal_indices(T, n, first_equal, err);
+        if (rc) return rc;
         for (int i = 0; i < n; i++) {
             const float* t = T + 16 * (size_t)i;
-            TriKey key;
-            for (int q = 0; q < 16; q++) {
-                if (!std::isfinite(t[q])) { err = "non-finite triangle data"; return PT_E_SCENE; }
-                float v = t[q] == 0.0f ? 0.0f : t[q];   // -0 == +0 for operator==
-                std::memcpy(&key.w[q], &v, 4);
-            }
-            first_equal[i] = first.emplace(key, i).first->second;
             Box b = empty_box();
             for (int vtx = 0; vtx < 3; vtx++)
                 for (int a = 0; a < 3; a++) {
@@ -618,7 +638,26 @@ thread_local std::string g_bvh_err;
 
 }  // namespace
 
+namespace pt_internal {
+void set_bvh_error(const std::string& msg) { g_bvh_err = msg; }
+}
+
 extern "C" {
+
+const char* pt_bvh_last_error(void) { return g_bvh_err.c_str(); }
+
+int pt_scene_build_bvh_gpu(pt_scene* s, int device) {
+    if (!s) return PT_E_ARG;
+    const int nt = (int)(s->tris.size() / 16);
+    if (nt <= 0) { s->err = "scene has no triangles (the reference indexes triangles[0])"; return PT_E_SCENE; }
+    int nn = 0;
+    std::vector<float> nodes(12 * (2 * (size_t)nt - 1));
+    const int rc = pt_bvh_build_gpu(s->tris.data(), nt, nodes.data(), 2 * nt - 1, &nn, device);
+    if (rc) { s->err = g_bvh_err; return rc; }
+    nodes.resize(12 * (size_t)nn);
+    s->nodes.swap(nodes);
+    return PT_OK;
+}
 
 int pt_bvh_build(const float* tris, int n_tris, float* nodes_out, int max_nodes, int* n_nodes) {
     if (!tris || n_tris <= 0 || !n_nodes) { g_bvh_err = "empty triangle list"; return PT_E_ARG; }

@@ -83,6 +83,9 @@ def lib():
             "pt_scene_last_error": (C.c_char_p, [vp]),
             "pt_scene_free": (None, [vp]),
             "pt_bvh_build": (ip, [_F, ip, _F, ip, C.POINTER(ip)]),
+            "pt_bvh_build_gpu": (ip, [_F, ip, _F, ip, C.POINTER(ip), ip]),
+            "pt_scene_build_bvh_gpu": (ip, [vp, ip]),
+            "pt_bvh_last_error": (C.c_char_p, []),
             "pt_aces_rgba8_host": (None, [_F, C.c_longlong, np.ctypeslib.ndpointer(np.uint8)]),
             "pt_create": (ip, [C.POINTER(_Config), C.POINTER(vp)]),
             "pt_destroy": (None, [vp]),
@@ -199,15 +202,21 @@ def load_obj_robust(obj_path, mtl_path=None):
     return a["tris"], a["mats"]
 
 
-def buildSAHTree(tris):
-    """bvh.h:255 -> nodes[K,12] {min, max, {tri0, tri1, hit, miss}} (preorder-pair layout)."""
+def buildSAHTree(tris, device=None):
+    """bvh.h:255 -> nodes[K,12] {min, max, {tri0, tri1, hit, miss}} (preorder-pair layout).
+    device: None = the host builder (pt_bvh_build), else the GPU builder on that device
+    (pt_bvh_build_gpu; the same output)."""
     tris = _f32(tris, 16)
     n = len(tris)
     out = np.zeros((max(2 * n, 1), 12), np.float32)
     nn = C.c_int()
-    rc = lib().pt_bvh_build(tris.reshape(-1) if n else np.zeros(16, np.float32), n, out.reshape(-1), len(out), C.byref(nn))
+    src = tris.reshape(-1) if n else np.zeros(16, np.float32)
+    if device is None:
+        rc = lib().pt_bvh_build(src, n, out.reshape(-1), len(out), C.byref(nn))
+    else:
+        rc = lib().pt_bvh_build_gpu(src, n, out.reshape(-1), len(out), C.byref(nn), int(device))
     if rc:
-        raise PTError(rc, lib().pt_scene_last_error(None).decode())
+        raise PTError(rc, lib().pt_bvh_last_error().decode())
     return out[: nn.value].copy()
 
 
