@@ -2605,7 +2605,7 @@ int pt_set_tuning(pt_ctx* c, int key, int value) {
         return PT_OK;
     }
     if (key == 4) {
-        if (value != 0 && (value < 32 || value > 1024)) return fail(c, PT_E_ARG, "pull batch must be 32..1024 (0 = auto)");
+        if (value < 0 || value > 1024) return fail(c, PT_E_ARG, "pull batch must be 1..1024 (0 = auto)");
         c->pull_batch = value;
         drop_graph(c);
         return PT_OK;
