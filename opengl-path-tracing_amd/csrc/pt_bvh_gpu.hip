@@ -245,6 +245,9 @@ thread_local std::string g_err;   // this builder's message, handed to pt_bvh_la
 inline unsigned blocks_for(long long n) { return (unsigned)((n + 255) / 256); }
 
 int build(const float* T, int n, int device, std::vector<DNode>& nodes) {
+    int prev_device = 0;
+    GCHK(hipGetDevice(&prev_device));
+    struct DeviceGuard { int d; ~DeviceGuard() { (void)hipSetDevice(d); } } dg{prev_device};   // the caller's device back
     GCHK(hipSetDevice(device));
     hipStream_t sm;
     GCHK(hipStreamCreateWithFlags(&sm, hipStreamNonBlocking));
