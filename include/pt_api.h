@@ -119,7 +119,8 @@ int pt_stats(pt_ctx* ctx, double* kernel_ms, unsigned long long out[5]);
  * phase (traversal step, leaf test, segment) the wave iterations and the active lanes
  * summed over them: [5] trav waves, [6] trav lanes, [7] leaf waves, [8] leaf lanes,
  * [9] segment waves, [10] segment lanes (persistent kernels; 0 for the tiled kernel),
- * [11] segments outside the exact-reciprocal guard (state-machine kernel). */
+ * [11] segments outside the exact-reciprocal guard (state-machine kernel); [15] 1 when the
+ * uploaded tree qualifies for the culling walk and it is on (tuning key 15), else 0. */
 int pt_stats_ex(pt_ctx* ctx, unsigned long long out[16]);
 /* Sum of render-kernel durations (HIP events on the render stream) and the number of
  * launches since the last reset; reset != 0 clears both after reading. */
@@ -157,6 +158,10 @@ int pt_set_kernel(pt_ctx* ctx, int variant);
  *         LDS-staged scenes, 40 for global-memory scenes),
  *         12 / 13 leaf / shade batch minimum (1..64, 0 = 64), 14 threads per workgroup
  *         (512, 768, 896, 1024; 0 = 1024).
+ * key 15 = culling walk (0 = automatic, 1 = off).  When the uploaded tree is a full binary
+ *         tree threaded in preorder whose internal boxes contain their children's, the
+ *         LDS-staged walk tests nodes with a cheaper conservative slab test and re-tests a
+ *         leaf's box exactly before one of its triangles may move t.
  * None of these change the image (each pixel's frames stay in order in one lane). */
 int pt_set_tuning(pt_ctx* ctx, int key, int value);
 

@@ -87,6 +87,8 @@ struct KParams {
     int wf_paths, wf_ring, wf_refill, wf_leaf_min, wf_shade_min;
     unsigned* wf_err;              // watchdog trips of the wavefront kernel (must stay 0)
     int shade_lds;                 // global-memory scene: materials + spheres staged in LDS too
+    int cons_walk;                 // LDS scene: the culling walk (slab_oct_cons, exact leaf re-test)
+    float cons_m[3];               // ... 2^-19 * the scene's largest |coordinate| per axis, rounded up
 };
 
 // Progressive mode (hipGraph replay): the frame range comes from a device counter, and
@@ -416,6 +418,7 @@ struct SceneView {
     const float4* mats;
     const float4* spheres;
     int np, tp;    // plane strides (float4) of the state-machine kernel's LDS copy
+    float cm[3];   // culling walk: 2^-19 * the scene's largest |coordinate| per axis (slab_oct_cons)
 };
 
 // Node / triangle-record access of the state-machine kernel.  Global memory holds AoS
@@ -514,6 +517,58 @@ __device__ __forceinline__ bool slab_oct(float4 A, float4 B, f3 o, f3 d, f3 rd, 
     float tn = fmaxf(fmaxf(xn, yn), zn);
     float tf = fminf(fminf(xf, yf), zf);
     return tn <= tf && tn <= cur_t;
+}
+
+// Conservative slab_oct of the culling walk.  Inside the exact-reciprocal
+// guard every quotient is finite and normal or zero.  With u = 2^-24, q = RN(RN(b - o) / d)
+// the exact quotient and rd = RN(1/d):
+//   PT_CONS_FMA = 0: q0 = RN(RN(b - o) * rd) lies within 4u |q| of q (three relative
+//                    roundings); lo = tn0 - 2^-20 |tn0| <= tn and hi = tf0 + 2^-20 |tf0| >= tf,
+//                    where tn0 / tf0 are the max / min of the near / far q0 (max and min only
+//                    select, so tn0 <= tn + 4.1u |tn| and tf0 >= tf - 4.1u |tf|);
+//   PT_CONS_FMA = 1: q0 = fma(b, rd, ord) with ord = RN(-o * rd) lies within
+//                    4.1u |q| + 1.1u |ord|; lo and hi as above, less / plus E = 2^-22 max|ord|;
+//   PT_CONS_FMA = 2 (default): the margin is folded into per-axis addends, no per-node
+//                    margin: near = fma(b, rd, ord - E_i), far = fma(b, rd, ord + E_i) with
+//                    E_i = 2^-19 M_i |rd_i| + 2^-17 |ord_i| (M_i: the largest |coordinate| of
+//                    the scene on axis i, so |b - o| <= M_i + |o_i| and
+//                    |q| <= M_i |rd_i| + 1.01 |ord_i|): the error of every fma quotient,
+//                    4.2u |q| + 2.1u |ord| + 2.1u E_i including the rounding of ord -+ E_i,
+//                    is below E_i, so near <= q_near and far >= q_far on every axis.
+// Either way an exact hit (tn <= tf and tn <= t) is always a hit here.  Only culling may use
+// it: a node it accepts and the exact test rejects is walked in vain, and a leaf reached
+// that way is rejected by the exact test of its own box, which the leaf phase runs before a
+// triangle moves t.
+#ifndef PT_CONS_FMA
+#define PT_CONS_FMA 2
+#endif
+#if PT_CONS_FMA != 2
+constexpr float kConsEta = 0x1p-20f;
+#endif
+// ol / oh: the per-ray addends (form 1: ord, ord; form 2: ord - E_i, ord + E_i); E: form 1's margin
+__device__ __forceinline__ bool slab_oct_cons(float4 A, float4 B, f3 o, f3 rd, f3 ol, f3 oh, float E, float cur_t) {
+#if PT_CONS_FMA
+    (void)o;
+    float xn = __builtin_fmaf(A.x, rd.x, ol.x), xf = __builtin_fmaf(A.y, rd.x, oh.x);
+    float yn = __builtin_fmaf(A.z, rd.y, ol.y), yf = __builtin_fmaf(A.w, rd.y, oh.y);
+    float zn = __builtin_fmaf(B.x, rd.z, ol.z), zf = __builtin_fmaf(B.y, rd.z, oh.z);
+#else
+    (void)ol;
+    (void)oh;
+    float xn = (A.x - o.x) * rd.x, xf = (A.y - o.x) * rd.x;
+    float yn = (A.z - o.y) * rd.y, yf = (A.w - o.y) * rd.y;
+    float zn = (B.x - o.z) * rd.z, zf = (B.y - o.z) * rd.z;
+#endif
+    float tn = fmaxf(fmaxf(xn, yn), zn);
+    float tf = fminf(fminf(xf, yf), zf);
+#if PT_CONS_FMA == 2
+    (void)E;
+    return tn <= tf && tn <= cur_t;
+#else
+    float lo = __builtin_fmaf(-kConsEta, __builtin_fabsf(tn), tn) - E;
+    float hi = __builtin_fmaf(kConsEta, __builtin_fabsf(tf), tf) + E;
+    return lo <= hi && lo <= cur_t;
+#endif
 }
 
 // Byte offset of the ray's octant image in the LDS walk: image k = sx | sy << 1 | sz << 2
@@ -1027,11 +1082,26 @@ constexpr int kWalkUnroll = PT_WALK_UNROLL;   // node steps per yield check of t
 // accepted scene -- pt_upload_scene rejects link graphs with a cycle, and a walk in an
 // acyclic graph visits each node at most once.  The transition is select-only; `leaf`
 // keeps the raw link (~code), decoded in LEAF.
-template <bool ALL_FAST, bool COUNT, bool LDS, bool PADN>
+// CONS (LDS scenes, never counting): the culling walk -- lanes inside the guard test every
+// node with slab_oct_cons; a leaf they stop at is re-tested exactly in the leaf phase.
+template <bool ALL_FAST, bool COUNT, bool LDS, bool PADN, bool CONS = false>
 __device__ __forceinline__ void trav_walk(const SceneView& S, f3 o, f3 d, f3 rd, bool fast, float t,
                                           unsigned long long live, int leaf_thresh, int shade_thresh,
                                           int trav_floor, int& st, int& bi, int& leaf, Cnt& c) {
     const int min_thresh = leaf_thresh < shade_thresh ? leaf_thresh : shade_thresh;
+    f3 ol = mk(0, 0, 0), oh = mk(0, 0, 0);
+    float E = 0.0f;
+    if (CONS && PT_CONS_FMA == 1) {
+        ol = oh = mk(-(o.x * rd.x), -(o.y * rd.y), -(o.z * rd.z));
+        E = 0x1p-22f * fmaxf(fmaxf(__builtin_fabsf(ol.x), __builtin_fabsf(ol.y)), __builtin_fabsf(ol.z));
+    } else if (CONS && PT_CONS_FMA == 2) {   // S.cm[i] = 2^-19 M_i (slab_oct_cons)
+        const f3 ord = mk(-(o.x * rd.x), -(o.y * rd.y), -(o.z * rd.z));
+        const f3 e = mk(__builtin_fmaf(S.cm[0], __builtin_fabsf(rd.x), 0x1p-17f * __builtin_fabsf(ord.x)),
+                        __builtin_fmaf(S.cm[1], __builtin_fabsf(rd.y), 0x1p-17f * __builtin_fabsf(ord.y)),
+                        __builtin_fmaf(S.cm[2], __builtin_fabsf(rd.z), 0x1p-17f * __builtin_fabsf(ord.z)));
+        ol = ord - e;
+        oh = ord + e;
+    }
     // Inside the walk one register carries the lane's state (WalkLinks): w >= 0 the next
     // node, w == -1 the chain ended (-> SHADE), w <= -2 stopped at the hit leaf with code
     // -2 - w (-> LEAF, bi = w).  st / bi are written back once at the end.
@@ -1044,7 +1114,9 @@ __device__ __forceinline__ void trav_walk(const SceneView& S, f3 o, f3 d, f3 rd,
             float4 lo, hi;
             node_at<LDS, PADN>(S, w, lo, hi);
             int a = __float_as_int(hi.z), b = __float_as_int(hi.w);
-            bool hb = (ALL_FAST || fast) ? (LDS ? slab_oct(lo, hi, o, d, rd, t) : slab_fast(lo, hi, o, d, rd, t))
+            bool hb = (ALL_FAST || fast) ? (LDS ? (CONS ? slab_oct_cons(lo, hi, o, rd, ol, oh, E, t)
+                                                        : slab_oct(lo, hi, o, d, rd, t))
+                                                 : slab_fast(lo, hi, o, d, rd, t))
                                          : slab(lo, hi, o, d, t);
             if (COUNT) { c.nodes++; diag_tick(c.tw, c.tl); }
 #ifdef PT_PHASE_CLOCK
@@ -1107,6 +1179,9 @@ __global__ __launch_bounds__(256, MINW) void k_render_sm(KParams p) {
         S.spheres = lds + nn + nt + nm;
         S.np = N;
         S.tp = T;
+        S.cm[0] = p.cons_m[0];
+        S.cm[1] = p.cons_m[1];
+        S.cm[2] = p.cons_m[2];
     } else {
         S.nodes = p.sc.nodes;     // reference layout; the walk image is for LDS only
         S.tris = p.sc.tris;
@@ -1442,9 +1517,27 @@ __global__ __launch_bounds__(256, MINW) void k_render_sm(KParams p) {
                 }
 #endif
             }
+            bool c1 = false, c2 = false;
             if (at) {
-                const bool c1 = (h1 > 0.0001f) & (h1 < t) & ((h1 < h2) | (h2 < 0.0001f));
-                const bool c2 = !c1 & (h2 > 0.0001f) & (h2 < t);
+                c1 = (h1 > 0.0001f) & (h1 < t) & ((h1 < h2) | (h2 < 0.0001f));
+                c2 = !c1 & (h2 > 0.0001f) & (h2 < t);
+            }
+            if (LDS && !COUNT && p.cons_walk) {
+                // the culling walk stopped here on the conservative test: the reference tests
+                // this leaf's triangles only if its box passes the exact test at this t, and
+                // only a triangle that moves t makes the difference (a leaf's hit and miss
+                // links are the same next-right).  Its image-0 offset: slot 2k+1 quad 3 .w.
+                const bool chk = at & fast & (c1 | c2);
+                if (__any(chk)) {
+                    if (chk) {
+                        float4 lo, hi;
+                        node_at<LDS, PADN>(S, __float_as_int(tri_quad<LDS>(S, s0 + 1, 3).w) + oct_base(d, S.np << 5),
+                                           lo, hi);
+                        if (!slab_oct(lo, hi, o, d, rd, t)) c1 = c2 = false;
+                    }
+                }
+            }
+            if (at) {
                 if (c1 | c2) {
                     t = c1 ? h1 : h2;
                     hprim = s0 + (c1 ? 0 : 1);
@@ -1458,10 +1551,17 @@ __global__ __launch_bounds__(256, MINW) void k_render_sm(KParams p) {
             // so a wave whose walking lanes are all inside the guard runs a walk without
             // the per-node IEEE-division branch.
             const unsigned long long live = __ballot(st != ST_DONE);
-            if (__all(fast || st != ST_TRAV))
+            const bool all_fast = __all(fast || st != ST_TRAV);
+            if (LDS && !COUNT && p.cons_walk) {    // the culling walk (kernel argument: uniform)
+                if (all_fast)
+                    trav_walk<true, COUNT, LDS, PADN, true>(S, o, d, rd, fast, t, live, p.leaf_thresh, p.shade_thresh, p.trav_floor, st, bi, leaf, c);
+                else
+                    trav_walk<false, COUNT, LDS, PADN, true>(S, o, d, rd, fast, t, live, p.leaf_thresh, p.shade_thresh, p.trav_floor, st, bi, leaf, c);
+            } else if (all_fast) {
                 trav_walk<true, COUNT, LDS, PADN>(S, o, d, rd, fast, t, live, p.leaf_thresh, p.shade_thresh, p.trav_floor, st, bi, leaf, c);
-            else
+            } else {
                 trav_walk<false, COUNT, LDS, PADN>(S, o, d, rd, fast, t, live, p.leaf_thresh, p.shade_thresh, p.trav_floor, st, bi, leaf, c);
+            }
         }
 #ifdef PT_PHASE_CLOCK
         clk[clk_ph] += clock64() - clk_t0;
@@ -2178,6 +2278,11 @@ struct pt_ctx {
     int n_nodes = 0, n_spheres = 0, n_mats = 0, n_slots = 0, scene_fast = 0, n_top = 0, walk_np = 1;
     float root_box[6] = {0, 0, 0, 0, 0, 0};
     int root_child = -1;
+    // the tree is a full binary tree threaded in preorder whose internal boxes contain their
+    // children's (nested_tree): the LDS walk may cull with slab_oct_cons (tuning key 15 = 1: off)
+    bool walk_nested = false;
+    int cons_off = 0;
+    float cons_m[3] = {0, 0, 0};   // KParams::cons_m
     size_t lds_bytes = 0;
     unsigned persist_blocks = 2048;
     // 0 = automatic: 52/44 when the scene is staged in LDS (best on C2 since the octant walk),
@@ -2229,6 +2334,40 @@ static int fail(pt_ctx* c, int code, const std::string& msg) {
         if (e_ != hipSuccess)                                                               \
             return fail(ctx, PT_E_HIP, std::string(#call ": ") + hipGetErrorString(e_));     \
     } while (0)
+
+// The structure the culling walk relies on, on the std140 records: from
+// the root, a full binary tree threaded in preorder -- an internal node's hit link is its
+// left child L, L's miss link its right child R, R's miss link the node's own -- in which
+// every internal box contains both children's boxes (exact float compares).  A walk that
+// enters a subtree the exact test would skip then leaves it at the same miss link, and any
+// leaf inside has a box within the skipped one, which fails the exact test too.
+static bool nested_tree(const float* bvh, int n_nodes) {
+    if (n_nodes <= 0) return false;
+    std::vector<unsigned char> seen(n_nodes, 0);
+    std::vector<std::pair<int, int>> st;   // (node, the miss link it must carry)
+    st.emplace_back(0, -1);
+    while (!st.empty()) {
+        const int x = st.back().first, after = st.back().second;
+        st.pop_back();
+        if (x < 0 || x >= n_nodes || seen[x]) return false;
+        seen[x] = 1;
+        const float* nd = bvh + 12 * (size_t)x;
+        if ((int)nd[11] != after) return false;
+        if (nd[8] > -1.0f) continue;               // leaf: hit == miss (checked by the caller)
+        const int l = (int)nd[10];
+        if (l < 0 || l >= n_nodes) return false;
+        const int r = (int)bvh[12 * (size_t)l + 11];
+        if (r < 0 || r >= n_nodes || r == after) return false;
+        for (int ch : {l, r}) {
+            const float* cb = bvh + 12 * (size_t)ch;
+            for (int q = 0; q < 3; q++)
+                if (!(nd[q] <= cb[q] && cb[4 + q] <= nd[4 + q])) return false;
+        }
+        st.emplace_back(r, after);
+        st.emplace_back(l, r);
+    }
+    return true;
+}
 
 static void free_scene(pt_ctx* c) {
     (void)hipFree(c->d_nodes); (void)hipFree(c->d_tris); (void)hipFree(c->d_mats); (void)hipFree(c->d_spheres);
@@ -2479,7 +2618,11 @@ int pt_upload_scene(pt_ctx* c, const float* tris, int n_tris, const float* bvh, 
             if (k & 4) std::swap(hi.x, hi.y);
             dwl[2 * N * k + i] = lo;
             dwl[2 * N * k + N + i] = hi;
-            if (leaf && k == 0) std::memcpy(&dt[8 * (size_t)slot_of[i] + 1].w, &hb, 4);
+            if (leaf && k == 0) {
+                std::memcpy(&dt[8 * (size_t)slot_of[i] + 1].w, &hb, 4);
+                const int self = 16 * i;           // the culling walk's exact leaf re-test
+                std::memcpy(&dt[8 * (size_t)slot_of[i] + 7].w, &self, 4);
+            }
         }
     }
     HIPCHK(c, hipStreamSynchronize(c->stream));   // a render in flight may still read the old scene
@@ -2512,6 +2655,13 @@ int pt_upload_scene(pt_ctx* c, const float* tris, int n_tris, const float* bvh, 
             if (!(nd[q] == 0.0f || (a >= 0x1p-40f && a <= 0x1p60f))) { c->scene_fast = 0; break; }
         }
         if (!(nd[0] <= nd[4] && nd[1] <= nd[5] && nd[2] <= nd[6])) c->scene_fast = 0;
+    }
+    c->walk_nested = nested_tree(bvh, n_nodes);
+    if (n_nodes > 0) {   // every box lies in the root box (nested): M_i bounds each |coordinate|
+        for (int q = 0; q < 3; q++) {
+            const double m = std::max(std::fabs((double)bvh[q]), std::fabs((double)bvh[4 + q]));
+            c->cons_m[q] = (float)std::ldexp(m * (1.0 + 0x1p-20), -19);   // rounded: within 2^-24 relative
+        }
     }
     c->walk_np = (int)N;
     c->lds_bytes = (size_t)(16 * N + 4 * c->n_slots + 3 * n_mats + 2 * n_spheres) * sizeof(float4);
@@ -2581,6 +2731,12 @@ int pt_set_tuning(pt_ctx* c, int key, int value) {
         } else {
             c->scratch_budget = (size_t)value << 20;
         }
+        drop_graph(c);
+        return PT_OK;
+    }
+    if (key == 15) {
+        if (value != 0 && value != 1) return fail(c, PT_E_ARG, "culling walk: 0 = automatic, 1 = off");
+        c->cons_off = value;
         drop_graph(c);
         return PT_OK;
     }
@@ -2780,6 +2936,8 @@ static int enqueue_render(pt_ctx* c, int frame_first, int n_frames, int acc_firs
     p.walk_np = c->walk_np;
     p.n_mats = c->n_mats;
     p.scene_fast = c->scene_fast;
+    p.cons_walk = c->walk_nested && !c->cons_off && !c->counting;
+    std::memcpy(p.cons_m, c->cons_m, sizeof(p.cons_m));
     std::memcpy(p.root_box, c->root_box, sizeof(p.root_box));
     p.root_child = c->root_child;
     {
@@ -3177,6 +3335,7 @@ extern "C" int pt_debug_wf_diag(unsigned long long out[16], int reset) {
 int pt_stats_ex(pt_ctx* c, unsigned long long out[16]) {
     if (!c || !out) return PT_E_ARG;
     std::memcpy(out, c->last_counts, sizeof(c->last_counts));
+    out[15] = c->walk_nested && !c->cons_off;   // the scene's LDS walk culls (slab_oct_cons)
     return PT_OK;
 }
 

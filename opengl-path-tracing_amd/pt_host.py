@@ -326,6 +326,11 @@ class PathTracer:
         if scratch_mib is not None:
             self._check(lib().pt_set_tuning(self.h, 8, int(scratch_mib)))
 
+    def set_culling(self, enable):
+        """Tuning key 15: the LDS walk's conservative culling (on by default where the tree
+        qualifies).  Never changes the image."""
+        self._check(lib().pt_set_tuning(self.h, 15, 0 if enable else 1))
+
     def set_key(self, key, value):
         """Raw pt_set_tuning(key, value) (experiments)."""
         self._check(lib().pt_set_tuning(self.h, int(key), int(value)))
@@ -380,7 +385,8 @@ class PathTracer:
         self._check(lib().pt_stats_ex(self.h, v))
         util = lambda w, l: float(v[l]) / max(1.0, 64.0 * float(v[w]))
         return dict(trav_iters=int(v[5]), trav_util=util(5, 6), leaf_iters=int(v[7]), leaf_util=util(7, 8),
-                    seg_iters=int(v[9]), seg_util=util(9, 10), slow_segments=int(v[11]), nan_segments=int(v[12]))
+                    seg_iters=int(v[9]), seg_util=util(9, 10), slow_segments=int(v[11]), nan_segments=int(v[12]),
+                    culling_walk=bool(v[15]))
 
     def copy_rows_device(self, dst_ptr, nbytes):
         self._check(lib().pt_copy_rows_device(self.h, C.c_void_p(dst_ptr), nbytes))

@@ -1,0 +1,118 @@
+"""The culling walk: the LDS walk tests nodes with a conservative slab test
+and re-tests a leaf's own box exactly before one of its triangles may move t.  On a tree that
+qualifies (a full binary tree threaded in preorder whose internal boxes contain their
+children's) the image is the reference's bit for bit; any other tree walks with the exact test.
+
+Tolerance: NONE -- uint32 bit patterns, as every parity test.
+"""
+import numpy as np
+import pytest
+
+import oracle_lib as O
+import pt_host as H
+
+pytestmark = pytest.mark.gpu
+
+
+def bits(a):
+    return np.ascontiguousarray(a, np.float32).view(np.uint32)
+
+
+def render(sc, W, Hh, n_frames, frame_first=1, culling=True, max_bounce=8, variant=0):
+    pt = H.PathTracer(W, Hh, max_bounce=max_bounce)
+    pt.set_kernel(variant)
+    pt.set_culling(culling)
+    pt.upload(sc)
+    active = pt.diag()["culling_walk"]
+    pt.render(frame_first, n_frames, 0)
+    img = pt.read_rgba32f()
+    pt.close()
+    return img, active
+
+
+def check(sc, label, W=64, Hh=48, n_frames=6, frame_first=1, expect_active=True):
+    want = O.render(sc, W, Hh, max_bounce=8, frame_first=frame_first, n_frames=n_frames)
+    for culling in (True, False):
+        got, active = render(sc, W, Hh, n_frames, frame_first, culling)
+        assert active == (culling and expect_active), (label, culling, active)
+        bad = int(np.count_nonzero(bits(got) != bits(want)))
+        assert bad == 0, "%s (culling %s): %d words differ" % (label, culling, bad)
+
+
+def preorder_depths(nodes):
+    """Depth of every node of a preorder-threaded tree (hit link = left child, the left
+    child's miss link = the right child)."""
+    depth = np.zeros(len(nodes), np.int64)
+    st = [(0, 0)]
+    while st:
+        x, dd = st.pop()
+        depth[x] = dd
+        if nodes[x, 8] <= -1.0:            # internal
+            left = int(nodes[x, 10])
+            right = int(nodes[left, 11])
+            st += [(left, dd + 1), (right, dd + 1)]
+    return depth
+
+
+def test_culling_on_benchmark_and_reference_scenes(cornell_scene, ship_scene):
+    check(cornell_scene, "cornell")
+    check(cornell_scene, "cornell, frames 3001..3006", frame_first=3001)
+    check(ship_scene, "ship")
+
+
+def test_culling_mid_size_lds_scene(tmp_path):
+    """A scene past the padded walk image (run-time plane stride)."""
+    import pt_scenes
+    sc = H.setupBuffers(*pt_scenes.write_scene("bunny", str(tmp_path), target_tris=80))
+    check(sc, "80-triangle LDS scene", n_frames=4)
+
+
+def test_loose_nested_boxes(cornell_scene):
+    """Boxes grown by an amount that shrinks with depth: still nested, no longer tight."""
+    sc = dict(cornell_scene)
+    nodes = np.array(sc["nodes"], np.float32)
+    depth = preorder_depths(nodes)
+    grow = (0.01 * (depth.max() + 1 - depth)).astype(np.float32)[:, None]
+    nodes[:, 0:3] -= grow
+    nodes[:, 4:7] += grow
+    sc["nodes"] = nodes
+    check(sc, "loose boxes")
+
+
+def test_not_nested_falls_back_to_exact(cornell_scene):
+    """A root box that no longer contains a child: the tree does not qualify, the walk uses
+    the exact test, and the image is still the reference's."""
+    sc = dict(cornell_scene)
+    nodes = np.array(sc["nodes"], np.float32)
+    left = int(nodes[0, 10])
+    nodes[0, 0] = np.float32(nodes[left, 0] + 0.25)    # the root's min.x inside its child's box
+    sc["nodes"] = nodes
+    check(sc, "not nested", expect_active=False)
+
+
+def test_far_from_origin(cornell_scene):
+    """Scene and camera translated far from the origin: |o| and the culling margins are large
+    against the box gaps."""
+    sc = dict(cornell_scene)
+    off = np.array([1000.0, -3000.0, 500.0], np.float32)
+    tris = np.array(sc["tris"], np.float32)
+    for v in (0, 4, 8):
+        tris[:, v:v + 3] += off
+    nodes = np.array(sc["nodes"], np.float32)
+    nodes[:, 0:3] += off
+    nodes[:, 4:7] += off
+    sph = np.array(sc["spheres"], np.float32).reshape(-1, 8)
+    sph[:, 0:3] += off
+    cam = np.array(sc["cam"], np.float32).reshape(12)
+    cam[0:3] += off
+    sc.update(tris=tris, nodes=nodes, spheres=sph, cam=cam)
+    check(sc, "translated scene")
+
+
+@pytest.mark.parametrize("variant", [2, 3, 4])
+def test_other_variants_ignore_the_setting(cornell_scene, variant):
+    """Only the state-machine kernel's LDS walk culls; the others are unchanged by key 15."""
+    want = O.render(cornell_scene, 40, 24, max_bounce=8, n_frames=3)
+    for culling in (True, False):
+        got, _ = render(cornell_scene, 40, 24, 3, culling=culling, variant=variant)
+        assert np.array_equal(bits(got), bits(want)), (variant, culling)
