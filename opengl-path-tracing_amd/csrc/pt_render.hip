@@ -2287,7 +2287,8 @@ struct pt_ctx {
     unsigned persist_blocks = 2048;
     // 0 = automatic: 52/44 when the scene is staged in LDS (best on C2 since the octant walk),
     // 16/24 when the walk reads global memory (re-swept after the leaf compaction: +2% on
-    // the C3 stand-in, +3% on C4 over 16/32); walk floor 8 / 6
+    // the C3 stand-in, +3% on C4 over 16/32); walk floor 3 / 6 (LDS: 8 until the culling walk
+    // made a walk step cheaper, then 2-4 measured +0.7% over 8)
     // (+0.8% on C2, +0.5% on C3 over no floor) -- tools/probe.py sweeps
     int leaf_thresh = 0, shade_thresh = 0, minw = 0, trav_floor = 0, compact_max = 63, pull_batch = 0;
     // frame-split work items (KParams::group): 0 = automatic, n = frames per item
@@ -2944,7 +2945,7 @@ static int enqueue_render(pt_ctx* c, int frame_first, int n_frames, int acc_firs
         bool lds_scene = c->lds_bytes <= kLdsSceneMax && c->variant != 3;
         p.leaf_thresh = c->leaf_thresh ? c->leaf_thresh : (lds_scene ? 52 : 16);
         p.shade_thresh = c->shade_thresh ? c->shade_thresh : (lds_scene ? 44 : 24);
-        p.trav_floor = c->trav_floor ? c->trav_floor : (lds_scene ? 8 : 6);
+        p.trav_floor = c->trav_floor ? c->trav_floor : (lds_scene ? 3 : 6);
         p.compact_max = c->compact_max;
     }
     p.rW = 1.0f / (float)p.W;
