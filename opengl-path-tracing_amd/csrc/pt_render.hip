@@ -40,6 +40,7 @@ struct DevScene {
     // the state-machine kernel's LDS image of the same tree (pt_upload_scene): node planes
     // with WalkLinks (byte offsets, 16 * index)
     const float4* walk_lds;
+    const float4* walk_sk;   // the culling walk's images: walk_lds with a ninth image of sinks
     const float4* tris;
     const float4* mats;
     const float4* spheres;
@@ -1070,6 +1071,12 @@ constexpr unsigned kPullBatch = 32;
 #ifndef PT_WALK_UNROLL
 #define PT_WALK_UNROLL 4
 #endif
+#ifndef PT_WALK_SINKS
+#define PT_WALK_SINKS 1     // the culling walk steps unmasked over its sink images
+#endif
+#ifndef PT_SINK_UNROLL
+#define PT_SINK_UNROLL 6    // its node steps per yield check (measured: 4 -2.2%, 8 -1.4% against 6)
+#endif
 constexpr int kWalkUnroll = PT_WALK_UNROLL;   // node steps per yield check of the walk (measured: 1 -> 2 +3.6%, 4 +5.7%, 6/8 slower)
 
 // The TRAV phase: each TRAV lane advances one node per iteration (bvh_intersect + the link
@@ -1105,10 +1112,45 @@ __device__ __forceinline__ void trav_walk(const SceneView& S, f3 o, f3 d, f3 rd,
     // Inside the walk one register carries the lane's state (WalkLinks): w >= 0 the next
     // node, w == -1 the chain ended (-> SHADE), w <= -2 stopped at the hit leaf with code
     // -2 - w (-> LEAF, bi = w).  st / bi are written back once at the end.
+    // The culling walk's images end in sinks instead (pt_upload_scene): w < sink0 walks,
+    // w == sink0 ended, w == sink0 + 16 (1 + k) stopped at leaf pair k; a stopped lane steps
+    // in place, so the step runs unmasked.
+    const int sink0 = (PADN ? kPadNodes : S.np) << 8;
     const bool walking = st == ST_TRAV;
     const unsigned long long mw = __ballot(walking);
     const unsigned long long pre_leaf = __ballot(st == ST_LEAF), pre_shade = __ballot(st == ST_SHADE);
-    int w = walking ? bi : -1;
+    int w = walking ? bi : (CONS ? sink0 : -1);
+#if PT_WALK_SINKS
+    if (CONS) {
+        auto sstep = [&]() {
+            float4 lo, hi;
+            node_at<LDS, PADN>(S, w, lo, hi);
+            const int a = __float_as_int(hi.z), b = __float_as_int(hi.w);
+            const bool hb = (ALL_FAST || fast) ? slab_oct_cons(lo, hi, o, rd, ol, oh, E, t) : slab(lo, hi, o, d, t);
+#ifdef PT_PHASE_CLOCK
+            if (w < sink0) diag_tick(c.tw, c.tl);
+#endif
+            w = hb ? a : b;
+        };
+        for (;;) {
+#pragma unroll
+            for (int u = 0; u < PT_SINK_UNROLL; u++) sstep();
+            unsigned long long mt = __ballot(w < sink0);
+            if (!mt) break;
+            if (__popcll(mt) < trav_floor) break;
+            if (__popcll(live & ~mt) >= min_thresh) {
+                if (__popcll(pre_leaf | __ballot(w > sink0)) >= leaf_thresh) break;
+                if (__popcll(pre_shade | (__ballot(w == sink0) & mw)) >= shade_thresh) break;
+            }
+        }
+        if (walking) {
+            st = w < sink0 ? ST_TRAV : (w == sink0 ? ST_SHADE : ST_LEAF);
+            bi = w;
+            leaf = ((w - sink0) >> 4) - 1;   // the leaf pair
+        }
+        return;
+    }
+#endif
     auto step = [&]() {
         if (w >= 0) {
             float4 lo, hi;
@@ -1166,9 +1208,13 @@ __global__ __launch_bounds__(256, MINW) void k_render_sm(KParams p) {
     if (LDS) {      // planes (see node_at / tri_quad)
         // node_at addresses LDS by raw offset: the dynamic LDS block must start at offset 0
         if ((unsigned)(size_t)(__attribute__((address_space(3))) const char*)g_lds != 0u) __builtin_trap();
-        const int N = PADN ? kPadNodes : p.walk_np, T = p.n_slots, nn = 16 * N, nt = 4 * T;   // 8 octant images
+        // 8 octant images (the culling walk: + its sink image)
+        const int N = PADN ? kPadNodes : p.walk_np, T = p.n_slots, nt = 4 * T;
+        const bool sk = PT_WALK_SINKS && !COUNT && p.cons_walk;
+        const int nn = sk ? 18 * N : 16 * N;
+        const float4* wsrc = sk ? p.sc.walk_sk : p.sc.walk_lds;
         const int nm = 3 * p.n_mats, ns = 2 * p.sc.n_spheres;
-        for (int i = threadIdx.x; i < nn; i += blockDim.x) lds[i] = p.sc.walk_lds[i];   // ready-made image
+        for (int i = threadIdx.x; i < nn; i += blockDim.x) lds[i] = wsrc[i];   // ready-made image
         for (int i = threadIdx.x; i < nt; i += blockDim.x) lds[nn + (i & 3) * T + (i >> 2)] = p.sc.tris[i];
         for (int i = threadIdx.x; i < nm; i += blockDim.x) lds[nn + nt + i] = p.sc.mats[i];
         for (int i = threadIdx.x; i < ns; i += blockDim.x) lds[nn + nt + nm + i] = p.sc.spheres[i];
@@ -1495,6 +1541,10 @@ __global__ __launch_bounds__(256, MINW) void k_render_sm(KParams p) {
                 const int code = LDS ? leaf : ~leaf;         // k << 2 | coplanar << 1 | single
                 s0 = (code >> 1) & ~1;                       // slots 2k, 2k+1
                 cop = (code & 2) != 0;
+                if (PT_WALK_SINKS && LDS && !COUNT && p.cons_walk) {   // sinks carry the pair k only
+                    s0 = 2 * leaf;
+                    cop = __float_as_int(tri_quad<LDS>(S, s0 + 1, 1).w) != 0;
+                }
                 nd0 = tri_quad<LDS>(S, s0, 0);               // {n, d0} of the first triangle
                 cont = LDS ? __float_as_int(tri_quad<LDS>(S, s0, 1).w) : bi;   // LDS: next-right, image 0
                 if (LDS && (fast & (cont >= 0))) cont += oct_base(d, S.np << 5);
@@ -2263,6 +2313,8 @@ struct pt_ctx {
     uchar4* rgba8 = nullptr;
     float4 *d_nodes = nullptr, *d_tris = nullptr, *d_mats = nullptr, *d_spheres = nullptr;
     float4* d_walk_lds = nullptr;   // LDS walk image (DevScene)
+    float4* d_walk_sk = nullptr;    // ... the culling walk's copy with its sink image
+    size_t lds_bytes_sk = 0;
     unsigned long long* d_counters = nullptr;
     unsigned int* d_work = nullptr;
     int* d_frame = nullptr;                      // progressive graph frame counter
@@ -2287,8 +2339,8 @@ struct pt_ctx {
     unsigned persist_blocks = 2048;
     // 0 = automatic: 52/44 when the scene is staged in LDS (best on C2 since the octant walk),
     // 16/24 when the walk reads global memory (re-swept after the leaf compaction: +2% on
-    // the C3 stand-in, +3% on C4 over 16/32); walk floor 3 / 6 (LDS: 8 until the culling walk
-    // made a walk step cheaper, then 2-4 measured +0.7% over 8)
+    // the C3 stand-in, +3% on C4 over 16/32); walk floor 5 / 6 (LDS: 8 until the culling walk
+    // made a walk step cheaper; re-swept with the sink walk: 5 +0.9% over 3, 2-8 within 1%)
     // (+0.8% on C2, +0.5% on C3 over no floor) -- tools/probe.py sweeps
     int leaf_thresh = 0, shade_thresh = 0, minw = 0, trav_floor = 0, compact_max = 63, pull_batch = 0;
     // frame-split work items (KParams::group): 0 = automatic, n = frames per item
@@ -2373,7 +2425,8 @@ static bool nested_tree(const float* bvh, int n_nodes) {
 static void free_scene(pt_ctx* c) {
     (void)hipFree(c->d_nodes); (void)hipFree(c->d_tris); (void)hipFree(c->d_mats); (void)hipFree(c->d_spheres);
     (void)hipFree(c->d_walk_lds);
-    c->d_nodes = c->d_tris = c->d_mats = c->d_spheres = c->d_walk_lds = nullptr;
+    (void)hipFree(c->d_walk_sk);
+    c->d_nodes = c->d_tris = c->d_mats = c->d_spheres = c->d_walk_lds = c->d_walk_sk = nullptr;
     c->scene_ok = false;
 }
 
@@ -2527,6 +2580,7 @@ int pt_upload_scene(pt_ctx* c, const float* tris, int n_tris, const float* bvh, 
             if (pos[i] < 0) pos[i] = nx++;
     }
     std::vector<int> slot_of(n_nodes, -1);   // leaf slot by device node index
+    std::vector<int> code_of(n_nodes, 0);    // leaf code by reference node index
     // --- transpose to device layouts
     std::vector<float4> dt(8 * (size_t)std::max(n_leaves, 1));
     auto put_tri = [&](float4* q, int ti) {
@@ -2563,6 +2617,7 @@ int pt_upload_scene(pt_ctx* c, const float* tris, int n_tris, const float* bvh, 
                 cop = A.x == B.x && A.y == B.y && A.z == B.z && A.w == B.w;
             }
             a = ~((s << 2) | (cop ? 2 : 0) | (t0 == t1 ? 1 : 0));
+            code_of[i] = ~a;
             b = (int)nd[11];
             slot_of[pos[i]] = s;
         } else {
@@ -2626,9 +2681,48 @@ int pt_upload_scene(pt_ctx* c, const float* tris, int n_tris, const float* bvh, 
             }
         }
     }
+    // The culling walk's copy of the walk images: the 8 octant images plus a
+    // ninth of "sinks" -- node records whose links both point to themselves.  A leaf's hit link
+    // leads to its sink (index 1 + k for leaf pair k) and the chain's end (-1) to sink 0, so a
+    // lane that stopped keeps stepping in place: the walk step needs no exec mask, and a lane
+    // walks while its position lies below the sink image.  A leaf's coplanar flag moves to
+    // slot 2k+1 quad 1 .w (the sink index carries only k).
+    std::vector<float4> dsk;
+    {
+        dsk.assign(18 * N, make_float4(0, 0, 0, 0));
+        std::copy(dwl.begin(), dwl.end(), dsk.begin());
+        const int sink0 = 16 * 2 * (int)N * 8;
+        for (int k = 0; k < 8; k++) {
+            for (int i = 0; i < n_nodes; i++) {
+                float4& hi = dsk[2 * N * k + N + i];
+                int a, b;
+                std::memcpy(&a, &hi.z, 4);
+                std::memcpy(&b, &hi.w, 4);
+                if (a <= -2) a = sink0 + 16 * (1 + ((-2 - a) >> 2));
+                if (b == -1) b = sink0;
+                std::memcpy(&hi.z, &a, 4);
+                std::memcpy(&hi.w, &b, 4);
+            }
+        }
+        for (int i = 0; i <= n_leaves; i++) {
+            const int self = sink0 + 16 * i;
+            float4 hi = make_float4(0, 0, 0, 0);
+            std::memcpy(&hi.z, &self, 4);
+            std::memcpy(&hi.w, &self, 4);
+            dsk[16 * N + N + i] = hi;
+        }
+        for (int i = 0; i < n_nodes; i++) {
+            const float* nd = bvh + 12 * (size_t)i;
+            if (!(nd[8] > -1.0f)) continue;
+            const int cop = (code_of[i] >> 1) & 1;
+            std::memcpy(&dt[8 * (size_t)leaf_slot[i] + 5].w, &cop, 4);
+        }
+    }
     HIPCHK(c, hipStreamSynchronize(c->stream));   // a render in flight may still read the old scene
     drop_graph(c);
     free_scene(c);
+    HIPCHK(c, hipMalloc(&c->d_walk_sk, dsk.size() * sizeof(float4)));
+    HIPCHK(c, hipMemcpy(c->d_walk_sk, dsk.data(), dsk.size() * sizeof(float4), hipMemcpyHostToDevice));
     HIPCHK(c, hipMalloc(&c->d_walk_lds, dwl.size() * sizeof(float4)));
     HIPCHK(c, hipMemcpy(c->d_walk_lds, dwl.data(), dwl.size() * sizeof(float4), hipMemcpyHostToDevice));
     HIPCHK(c, hipMalloc(&c->d_nodes, dn.size() * sizeof(float4)));
@@ -2666,6 +2760,7 @@ int pt_upload_scene(pt_ctx* c, const float* tris, int n_tris, const float* bvh, 
     }
     c->walk_np = (int)N;
     c->lds_bytes = (size_t)(16 * N + 4 * c->n_slots + 3 * n_mats + 2 * n_spheres) * sizeof(float4);
+    c->lds_bytes_sk = c->lds_bytes + 2 * N * sizeof(float4);
     c->root_child = -1;
     if (n_nodes > 0) {
         const float4 r0 = dn[0], r1 = dn[1];
@@ -2938,6 +3033,7 @@ static int enqueue_render(pt_ctx* c, int frame_first, int n_frames, int acc_firs
     p.n_mats = c->n_mats;
     p.scene_fast = c->scene_fast;
     p.cons_walk = c->walk_nested && !c->cons_off && !c->counting;
+    p.sc.walk_sk = c->d_walk_sk;
     std::memcpy(p.cons_m, c->cons_m, sizeof(p.cons_m));
     std::memcpy(p.root_box, c->root_box, sizeof(p.root_box));
     p.root_child = c->root_child;
@@ -2945,7 +3041,7 @@ static int enqueue_render(pt_ctx* c, int frame_first, int n_frames, int acc_firs
         bool lds_scene = c->lds_bytes <= kLdsSceneMax && c->variant != 3;
         p.leaf_thresh = c->leaf_thresh ? c->leaf_thresh : (lds_scene ? 52 : 16);
         p.shade_thresh = c->shade_thresh ? c->shade_thresh : (lds_scene ? 44 : 24);
-        p.trav_floor = c->trav_floor ? c->trav_floor : (lds_scene ? 3 : 6);
+        p.trav_floor = c->trav_floor ? c->trav_floor : (lds_scene ? 5 : 6);
         p.compact_max = c->compact_max;
     }
     p.rW = 1.0f / (float)p.W;
@@ -3026,7 +3122,7 @@ static int enqueue_render(pt_ctx* c, int frame_first, int n_frames, int acc_firs
     } else {
         // persistent grid: enough resident waves to fill every SIMD; surplus blocks find the
         // queue empty and exit.  Never more blocks than 8x8 tiles (64 lanes per tile).
-        size_t lds = use_lds ? c->lds_bytes : 0;
+        size_t lds = use_lds ? ((PT_WALK_SINKS && p.cons_walk) ? c->lds_bytes_sk : c->lds_bytes) : 0;
         unsigned tiles = (unsigned)(((p.W + 7) / 8) * ((c->rows_local + 7) / 8));
         unsigned items = tiles * (unsigned)((n_frames + p.group - 1) / p.group);   // 64-lane items
         unsigned blocks = std::min<unsigned>(c->persist_blocks, std::max(1u, (items + 3) / 4));
