@@ -2688,7 +2688,8 @@ int pt_upload_scene(pt_ctx* c, const float* tris, int n_tris, const float* bvh, 
     // walks while its position lies below the sink image.  A leaf's coplanar flag moves to
     // slot 2k+1 quad 1 .w (the sink index carries only k).
     std::vector<float4> dsk;
-    {
+    const bool nested = nested_tree(bvh, n_nodes);
+    if (nested) {
         dsk.assign(18 * N, make_float4(0, 0, 0, 0));
         std::copy(dwl.begin(), dwl.end(), dsk.begin());
         const int sink0 = 16 * 2 * (int)N * 8;
@@ -2721,8 +2722,10 @@ int pt_upload_scene(pt_ctx* c, const float* tris, int n_tris, const float* bvh, 
     HIPCHK(c, hipStreamSynchronize(c->stream));   // a render in flight may still read the old scene
     drop_graph(c);
     free_scene(c);
-    HIPCHK(c, hipMalloc(&c->d_walk_sk, dsk.size() * sizeof(float4)));
-    HIPCHK(c, hipMemcpy(c->d_walk_sk, dsk.data(), dsk.size() * sizeof(float4), hipMemcpyHostToDevice));
+    if (nested) {
+        HIPCHK(c, hipMalloc(&c->d_walk_sk, dsk.size() * sizeof(float4)));
+        HIPCHK(c, hipMemcpy(c->d_walk_sk, dsk.data(), dsk.size() * sizeof(float4), hipMemcpyHostToDevice));
+    }
     HIPCHK(c, hipMalloc(&c->d_walk_lds, dwl.size() * sizeof(float4)));
     HIPCHK(c, hipMemcpy(c->d_walk_lds, dwl.data(), dwl.size() * sizeof(float4), hipMemcpyHostToDevice));
     HIPCHK(c, hipMalloc(&c->d_nodes, dn.size() * sizeof(float4)));
@@ -2751,7 +2754,7 @@ int pt_upload_scene(pt_ctx* c, const float* tris, int n_tris, const float* bvh, 
         }
         if (!(nd[0] <= nd[4] && nd[1] <= nd[5] && nd[2] <= nd[6])) c->scene_fast = 0;
     }
-    c->walk_nested = nested_tree(bvh, n_nodes);
+    c->walk_nested = nested;
     if (n_nodes > 0) {   // every box lies in the root box (nested): M_i bounds each |coordinate|
         for (int q = 0; q < 3; q++) {
             const double m = std::max(std::fabs((double)bvh[q]), std::fabs((double)bvh[4 + q]));
