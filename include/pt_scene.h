@@ -77,6 +77,11 @@ int pt_bvh_build_gpu(const float* tris, int n_tris, float* nodes_out, int max_no
                      int device);
 /* pt_scene_build_bvh with the GPU builder. */
 int pt_scene_build_bvh_gpu(pt_scene* s, int device);
+/* 1 when the threaded tree qualifies for the culling walk: from node 0 a
+ * full binary tree threaded in preorder (hit link = left child, the left child's miss link =
+ * the right child, the right child's miss link = the parent's) whose internal boxes contain
+ * both children's boxes exactly; else 0.  Host only; pt_upload_scene applies the same check. */
+int pt_bvh_culling_ok(const float* nodes, int n_nodes);
 /* Message of the calling thread's last pt_bvh_build / pt_bvh_build_gpu failure. */
 const char* pt_bvh_last_error(void);
 

@@ -22,6 +22,7 @@
 //   sphere 32 B: {c.xyz, r*r}, {matIdx, 0, 0, 0}
 #include "pt_math.h"
 #include "../../include/pt_api.h"
+#include "../../include/pt_scene.h"
 
 #include <hip/hip_runtime.h>
 
@@ -2503,6 +2504,10 @@ void pt_destroy(pt_ctx* c) {
 }
 
 const char* pt_last_error(const pt_ctx* c) { return c ? c->err.c_str() : "null context"; }
+
+int pt_bvh_culling_ok(const float* nodes, int n_nodes) {
+    return nodes && n_nodes > 0 && nested_tree(nodes, n_nodes) ? 1 : 0;
+}
 
 int pt_upload_scene(pt_ctx* c, const float* tris, int n_tris, const float* bvh, int n_nodes,
                     const float* mats, int n_mats, const float* spheres, int n_spheres) {

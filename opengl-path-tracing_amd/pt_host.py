@@ -86,6 +86,7 @@ def lib():
             "pt_bvh_build_gpu": (ip, [_F, ip, _F, ip, C.POINTER(ip), ip]),
             "pt_scene_build_bvh_gpu": (ip, [vp, ip]),
             "pt_bvh_last_error": (C.c_char_p, []),
+            "pt_bvh_culling_ok": (ip, [_F, ip]),
             "pt_aces_rgba8_host": (None, [_F, C.c_longlong, np.ctypeslib.ndpointer(np.uint8)]),
             "pt_create": (ip, [C.POINTER(_Config), C.POINTER(vp)]),
             "pt_destroy": (None, [vp]),
@@ -251,6 +252,12 @@ def scene_from_arrays(tris, mats, builtins=True, camera=None):
     a = s.arrays()
     a["cam"] = DEFAULT_CAMERA.copy() if camera is None else np.asarray(camera, np.float32).reshape(12)
     return SceneBuffers(a)
+
+
+def bvh_culling_ok(nodes):
+    """pt_bvh_culling_ok: does the threaded tree qualify for the culling walk?"""
+    n = _f32(nodes, 12)
+    return bool(lib().pt_bvh_culling_ok(n.reshape(-1) if len(n) else np.zeros(12, np.float32), len(n)))
 
 
 def aces_rgba8_host(img):
