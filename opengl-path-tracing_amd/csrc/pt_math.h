@@ -61,11 +61,13 @@ PT_HD float rcp_fast(float x) {
 }
 PT_HD float sqrt_fast(float x) {
 #if defined(__HIP_DEVICE_COMPILE__)
-    float s = __builtin_amdgcn_sqrtf(x);
-    float sd = __uint_as_float(__float_as_uint(s) - 1u), su = __uint_as_float(__float_as_uint(s) + 1u);
-    float rd = __builtin_fmaf(-sd, s, x), ru = __builtin_fmaf(-su, s, x);
-    s = rd <= 0.0f ? sd : s;
-    return ru > 0.0f ? su : s;
+    // v_rsq_f32, s0 = x * y, and one fma correction s0 + (x - s0^2) * y/2: 5 VALU (the
+    // former v_sqrt_f32 + neighbour-residual selects took 9); correctly rounded for every x
+    // in the guard on gfx950 (tools/verify_fastmath.hip, exhaustive)
+    const float y = __builtin_amdgcn_rsqf(x);
+    const float s0 = x * y, h = 0.5f * y;
+    const float r = __builtin_fmaf(-s0, s0, x);
+    return __builtin_fmaf(r, h, s0);
 #else
     return sqrtf(x);
 #endif
