@@ -287,7 +287,10 @@ PT_HD float random_normal(uint32_t& s) {            // :115-120 (theta first, th
     float u2 = random01(s);
     return __builtin_sqrtf(-1.3862944f * __builtin_amdgcn_logf(u2)) * __builtin_amdgcn_cosf(u1);
 #endif
-    float theta = (2.0f * 3.1415926f) * random01(s);
+    // (2 * 3.1415926f) * (float(r) * 2^-32) as ONE rounding: float(r) * 2^-32 is exact (r >= 1
+    // or 0: no subnormal) and so is the constant's 2^-32 scaling, so both forms round the same
+    // real product
+    float theta = (float)next_random(s) * ((2.0f * 3.1415926f) * (1.0f / 4294967296.0f));
 #if defined(__HIP_DEVICE_COMPILE__)
     float rho = sqrt_g(-2.0f * logf_bf(random01(s)));
     return rho * cosf_bf(theta);
