@@ -2339,8 +2339,9 @@ struct pt_ctx {
     size_t lds_bytes = 0;
     unsigned persist_blocks = 2048;
     // 0 = automatic: 52/44 when the scene is staged in LDS (best on C2 since the octant walk),
-    // 16/24 when the walk reads global memory (re-swept after the leaf compaction: +2% on
-    // the C3 stand-in, +3% on C4 over 16/32); walk floor 5 / 6 (LDS: 8 until the culling walk
+    // 20/24 when the walk reads global memory (re-swept after the leaf compaction: +2% on
+    // the C3 stand-in, +3% on C4 over 16/32; leaf 20 re-swept in round 2: C3 +1.3%, C4 +0.6%
+    // over 16); walk floor 5 / 6 (LDS: 8 until the culling walk
     // made a walk step cheaper; re-swept with the sink walk: 5 +0.9% over 3, 2-8 within 1%)
     // (+0.8% on C2, +0.5% on C3 over no floor) -- tools/probe.py sweeps
     int leaf_thresh = 0, shade_thresh = 0, minw = 0, trav_floor = 0, compact_max = 63, pull_batch = 0;
@@ -3047,7 +3048,7 @@ static int enqueue_render(pt_ctx* c, int frame_first, int n_frames, int acc_firs
     p.root_child = c->root_child;
     {
         bool lds_scene = c->lds_bytes <= kLdsSceneMax && c->variant != 3;
-        p.leaf_thresh = c->leaf_thresh ? c->leaf_thresh : (lds_scene ? 52 : 16);
+        p.leaf_thresh = c->leaf_thresh ? c->leaf_thresh : (lds_scene ? 52 : 20);
         p.shade_thresh = c->shade_thresh ? c->shade_thresh : (lds_scene ? 44 : 24);
         p.trav_floor = c->trav_floor ? c->trav_floor : (lds_scene ? 5 : 6);
         p.compact_max = c->compact_max;
