@@ -116,3 +116,29 @@ def test_other_variants_ignore_the_setting(cornell_scene, variant):
     for culling in (True, False):
         got, _ = render(cornell_scene, 40, 24, 3, culling=culling, variant=variant)
         assert np.array_equal(bits(got), bits(want)), (variant, culling)
+
+
+def test_culling_key_validation_and_graph(cornell_scene):
+    """Tuning key 15 accepts 0 / 1 only; switching it drops a captured progressive graph
+    (the graph bakes the walk in), and the recaptured loop is the reference's image either
+    way."""
+    want = O.render(cornell_scene, 40, 24, max_bounce=8, n_frames=8)
+    pt = H.PathTracer(40, 24, max_bounce=8)
+    try:
+        pt.upload(cornell_scene)
+        with pytest.raises(H.PTError):
+            pt.set_key(15, 2)
+        pt.progressive_setup(4, 2)
+        pt.progressive_run(1)
+        assert np.array_equal(bits(pt.read_rgba32f()), bits(want))
+        pt.set_culling(False)
+        with pytest.raises(H.PTError) as e:
+            pt.progressive_run(1)
+        assert e.value.code == -6     # PT_E_STATE: set up again first
+        pt.progressive_setup(4, 2)
+        pt.progressive_reset(1)
+        pt.progressive_run(1)
+        assert np.array_equal(bits(pt.read_rgba32f()), bits(want))
+        assert not pt.diag()["culling_walk"]
+    finally:
+        pt.close()
