@@ -119,8 +119,11 @@ int pt_stats(pt_ctx* ctx, double* kernel_ms, unsigned long long out[5]);
  * phase (traversal step, leaf test, segment) the wave iterations and the active lanes
  * summed over them: [5] trav waves, [6] trav lanes, [7] leaf waves, [8] leaf lanes,
  * [9] segment waves, [10] segment lanes (persistent kernels; 0 for the tiled kernel),
- * [11] segments outside the exact-reciprocal guard (state-machine kernel); [15] 1 when the
- * uploaded tree qualifies for the culling walk and it is on (tuning key 15), else 0. */
+ * [11] segments outside the exact-reciprocal guard (state-machine kernel), [12] segments
+ * that met a NaN.  Scene facts (any build): [13] bytes of the LDS scene copy, [14] the same
+ * with the culling walk's sink image (0 when the tree does not qualify); [15] 1 when the
+ * uploaded tree qualifies for the culling walk, it is on (tuning key 15) and the sink image
+ * costs no resident workgroup per CU at the set waves per SIMD (key 3), else 0. */
 int pt_stats_ex(pt_ctx* ctx, unsigned long long out[16]);
 /* Sum of render-kernel durations (HIP events on the render stream) and the number of
  * launches since the last reset; reset != 0 clears both after reading. */

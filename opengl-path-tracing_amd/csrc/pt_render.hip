@@ -3003,6 +3003,19 @@ static int launch_frames(const pt_ctx* c, int n_frames) {
     }
 }
 
+// Whether the state-machine kernel's LDS walk culls: the tree qualifies
+// (walk_nested), key 15 leaves it on, nothing is counted, and the sink image (32 B per node
+// beside the 16 N octant records) costs no resident block -- a scene whose copy just fits
+// mw blocks per CU in 160 KiB would otherwise lose a block per CU, far more than the walk
+// gains (+7%).
+static bool cons_walk_on(const pt_ctx* c) {
+    if (!c->walk_nested || c->cons_off || c->counting) return false;
+    if (!PT_WALK_SINKS) return true;
+    const size_t mw = (size_t)(c->minw ? c->minw : 7);
+    const auto blocks = [mw](size_t b) { return b ? std::min(mw, (size_t)(160 * 1024) / b) : mw; };
+    return blocks(c->lds_bytes_sk) >= blocks(c->lds_bytes);
+}
+
 // Enqueues one render launch (work-queue reset + kernel) on the context stream.  With
 // `frame_dev` the frame range is read on the device (progressive graph replay).
 static int enqueue_render(pt_ctx* c, int frame_first, int n_frames, int acc_first, const int* frame_dev,
@@ -3041,7 +3054,7 @@ static int enqueue_render(pt_ctx* c, int frame_first, int n_frames, int acc_firs
     p.walk_np = c->walk_np;
     p.n_mats = c->n_mats;
     p.scene_fast = c->scene_fast;
-    p.cons_walk = c->walk_nested && !c->cons_off && !c->counting;
+    p.cons_walk = cons_walk_on(c);
     p.sc.walk_sk = c->d_walk_sk;
     std::memcpy(p.cons_m, c->cons_m, sizeof(p.cons_m));
     std::memcpy(p.root_box, c->root_box, sizeof(p.root_box));
@@ -3441,7 +3454,9 @@ extern "C" int pt_debug_wf_diag(unsigned long long out[16], int reset) {
 int pt_stats_ex(pt_ctx* c, unsigned long long out[16]) {
     if (!c || !out) return PT_E_ARG;
     std::memcpy(out, c->last_counts, sizeof(c->last_counts));
-    out[15] = c->walk_nested && !c->cons_off;   // the scene's LDS walk culls (slab_oct_cons)
+    out[13] = c->lds_bytes;
+    out[14] = c->walk_nested ? c->lds_bytes_sk : 0;
+    out[15] = cons_walk_on(c);               // the scene's LDS walk culls (slab_oct_cons)
     return PT_OK;
 }
 

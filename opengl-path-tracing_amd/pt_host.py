@@ -393,7 +393,7 @@ class PathTracer:
         util = lambda w, l: float(v[l]) / max(1.0, 64.0 * float(v[w]))
         return dict(trav_iters=int(v[5]), trav_util=util(5, 6), leaf_iters=int(v[7]), leaf_util=util(7, 8),
                     seg_iters=int(v[9]), seg_util=util(9, 10), slow_segments=int(v[11]), nan_segments=int(v[12]),
-                    culling_walk=bool(v[15]))
+                    lds_bytes=int(v[13]), lds_bytes_sinks=int(v[14]), culling_walk=bool(v[15]))
 
     def copy_rows_device(self, dst_ptr, nbytes):
         self._check(lib().pt_copy_rows_device(self.h, C.c_void_p(dst_ptr), nbytes))

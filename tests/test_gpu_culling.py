@@ -142,3 +142,49 @@ def test_culling_key_validation_and_graph(cornell_scene):
         assert not pt.diag()["culling_walk"]
     finally:
         pt.close()
+
+
+def blocks_per_cu(lds, mw):
+    return min(mw, 160 * 1024 // lds) if lds else mw
+
+
+def test_sink_image_never_costs_a_workgroup(cornell_scene, tmp_path):
+    """The sink image adds 32 B per node to the LDS copy; the walk culls only while that
+    leaves the resident workgroups per CU unchanged at the set waves per SIMD (key 3).  Scan
+    scene sizes for one the rule turns off, and render it exactly either way."""
+    import pt_scenes
+    pt = H.PathTracer(48, 32, max_bounce=8)
+    found, seen = None, []
+    try:
+        for target in range(2, 120, 2):
+            sc = H.setupBuffers(*pt_scenes.write_scene("bunny", str(tmp_path / str(target)), target_tris=target))
+            pt.upload(sc)
+            d = pt.diag()
+            seen.append((target, len(sc["tris"]) // 16 if np.ndim(sc["tris"]) == 1 else len(sc["tris"]),
+                         d["lds_bytes"], d["lds_bytes_sinks"]))
+            if d["lds_bytes_sinks"] == 0 or d["lds_bytes"] > 48 * 1024:
+                continue
+            for ws in (0, 5, 6, 7, 8):
+                pt.set_key(3, ws)
+                mw = ws or 7
+                want_on = blocks_per_cu(d["lds_bytes_sinks"], mw) >= blocks_per_cu(d["lds_bytes"], mw)
+                assert pt.diag()["culling_walk"] == want_on, (target, ws, d)
+                if not want_on and found is None:
+                    found = (sc, ws)
+            pt.set_key(3, 0)
+            if d["lds_bytes"] > 48 * 1024:
+                break
+    finally:
+        pt.close()
+    assert found is not None, "no scene size in the scan hits the occupancy rule: %s" % seen
+    sc, ws = found
+    want = O.render(sc, 32, 24, max_bounce=8, n_frames=3)
+    pt = H.PathTracer(32, 24, max_bounce=8)
+    try:
+        pt.set_key(3, ws)
+        pt.upload(sc)
+        assert not pt.diag()["culling_walk"]
+        pt.render(1, 3, 0)
+        assert np.array_equal(bits(pt.read_rgba32f()), bits(want))
+    finally:
+        pt.close()
