@@ -1201,8 +1201,8 @@ __device__ __forceinline__ void trav_walk(const SceneView& S, f3 o, f3 d, f3 rd,
 __device__ unsigned long long g_phase_clk[8];
 #endif
 
-template <bool COUNT, bool LDS, int MINW, bool MULTI, bool SPLIT, bool PADN = false>
-__global__ __launch_bounds__(256, MINW) void k_render_sm(KParams p) {
+template <bool COUNT, bool LDS, int MINW, bool MULTI, bool SPLIT, bool PADN = false, int NT = 256>
+__global__ __launch_bounds__(NT, MINW) void k_render_sm(KParams p) {
     resolve_frames(p);
     extern __shared__ float4 lds[];
     SceneView S;
@@ -2297,7 +2297,18 @@ __global__ __launch_bounds__(256) void k_aces(const float4* __restrict__ src, uc
 }  // namespace
 
 // ===================================================================== host side
-constexpr size_t kLdsSceneMax = 48 * 1024;   // stage the scene in LDS up to 48 KiB
+// Stage the scene in LDS up to this size.  One workgroup may hold all 160 KiB of a CU's LDS
+// on gfx950; a copy too large for the resident waves' worth of 256-thread workgroups is
+// shared by wider ones (lds_threads), so mid-size scenes keep the LDS walk at 4+ waves per
+// SIMD instead of the global-memory walk.
+#ifndef PT_LDS_SCENE_MAX_KIB
+#define PT_LDS_SCENE_MAX_KIB 152
+#endif
+#ifndef PT_LDS_WIDE
+#define PT_LDS_WIDE 1
+#endif
+constexpr size_t kLdsSceneMax = (size_t)PT_LDS_SCENE_MAX_KIB * 1024;
+constexpr size_t kLdsSceneSmall = 48 * 1024;  // staged by 256-thread workgroups in every configuration
 // global-memory scenes: the first kTopNodes device nodes (breadth-first from the root) are
 // staged in LDS, 24 KiB per workgroup (6 workgroups per CU stay resident)
 constexpr int kTopNodes = 768;
@@ -2910,13 +2921,22 @@ int pt_set_tuning(pt_ctx* c, int key, int value) {
 // accumulates in registers).  The counting build follows the same plan: with whole-pixel
 // items a 1080p/8 share of a 1024-frame launch would run each lane through 1024 frames
 // in sequence (minutes).
+// Whether the state-machine kernel (variants 0 and 4's fallback) stages the scene in LDS:
+// up to kLdsSceneSmall always; up to kLdsSceneMax when wide workgroups share the copy
+// (lds_threads' configuration).  Variant 3 forces the global-memory walk.
+static bool lds_staged(const pt_ctx* c) {
+    if (c->variant == 3) return false;
+    if (c->lds_bytes <= kLdsSceneSmall) return true;
+    return PT_LDS_WIDE && !c->counting && !c->minw && c->cfg.rays_per_pixel == 1 && c->lds_bytes <= kLdsSceneMax;
+}
+
 static int plan_group(const pt_ctx* c, int n_frames) {
     if (c->variant != 0 && c->variant != 3 && c->variant != 4) return n_frames;
     if (c->group_force > 0) return std::min(c->group_force, n_frames);
     const int waves = c->minw ? c->minw : 6;
     const double lanes = (double)c->n_cu * 4.0 * waves * 64.0;
     const double px = (double)c->rows_local * c->cfg.width;
-    const bool lds_scene = c->lds_bytes <= kLdsSceneMax && c->variant != 3;
+    const bool lds_scene = lds_staged(c);
     int g = (int)(px * n_frames / (16.0 * lanes));
     g = std::max(1, std::min(g, lds_scene ? 16 : 4));  // C2: 16 +0.5% over 8; C3 stand-in: 4 +8% over 8
     return std::min(g, n_frames);
@@ -2961,7 +2981,7 @@ static int wf_threads(const pt_ctx* c) { return c->wf_threads ? c->wf_threads : 
 // LDS bytes of variant 4's scene part: an LDS-staged scene as variant 0 stages it; for a
 // global-memory scene the top nodes plus materials and spheres (-1: these do not fit).
 static long long wf_scene_bytes(const pt_ctx* c) {
-    if (c->lds_bytes <= kLdsSceneMax) return (long long)c->lds_bytes;
+    if (c->lds_bytes <= kLdsSceneSmall) return (long long)c->lds_bytes;
     const long long shade = (3LL * c->n_mats + 2LL * c->n_spheres) * 16;
     if (shade > 4096) return -1;
     return (long long)c->n_top * 32 + shade;
@@ -3016,6 +3036,23 @@ static bool cons_walk_on(const pt_ctx* c) {
     return blocks(c->lds_bytes_sk) >= blocks(c->lds_bytes);
 }
 
+// Threads per workgroup of the state-machine kernel on an LDS-staged scene of `lds` bytes:
+// the k = 1..4 waves per SIMD per workgroup that make the most resident waves, min(floor(160
+// KiB / lds), floor(7 / k)) * k (7 waves per SIMD is the kernel's register budget), the
+// narrowest on a tie: 256 threads down to a 23 KiB copy, then 512 / 768 / 1024 (6, 6, 4 waves
+// per SIMD at 32 / 54 / 160 KiB).  The wide instantiations are the default configuration's (non-counting, one ray
+// per pixel, automatic occupancy); other launches keep 256 threads.
+static int lds_threads(const pt_ctx* c, size_t lds) {
+    if (!PT_LDS_WIDE || c->counting || c->minw || c->cfg.rays_per_pixel > 1 || !lds) return 256;
+    const int per_cu = (int)((size_t)(160 * 1024) / lds);     // copies resident per CU
+    int best_k = 1, best = 0;
+    for (int k = 1; k <= 4; k++) {      // k waves per SIMD per workgroup, at most 7 per SIMD
+        const int waves = std::min(per_cu, 7 / k) * k;
+        if (waves > best) { best = waves; best_k = k; }
+    }
+    return 256 * best_k;
+}
+
 // Enqueues one render launch (work-queue reset + kernel) on the context stream.  With
 // `frame_dev` the frame range is read on the device (progressive graph replay).
 static int enqueue_render(pt_ctx* c, int frame_first, int n_frames, int acc_first, const int* frame_dev,
@@ -3060,7 +3097,7 @@ static int enqueue_render(pt_ctx* c, int frame_first, int n_frames, int acc_firs
     std::memcpy(p.root_box, c->root_box, sizeof(p.root_box));
     p.root_child = c->root_child;
     {
-        bool lds_scene = c->lds_bytes <= kLdsSceneMax && c->variant != 3;
+        bool lds_scene = lds_staged(c);
         p.leaf_thresh = c->leaf_thresh ? c->leaf_thresh : (lds_scene ? 52 : 20);
         p.shade_thresh = c->shade_thresh ? c->shade_thresh : (lds_scene ? 44 : 24);
         p.trav_floor = c->trav_floor ? c->trav_floor : (lds_scene ? 5 : 6);
@@ -3079,7 +3116,7 @@ static int enqueue_render(pt_ctx* c, int frame_first, int n_frames, int acc_firs
     // items and the global-memory scenes' long segments keep 32 (C3 stand-in, one frame per
     // launch: 3.19 ms with 32, 3.63 with 128).  Tuning key 4 overrides.
     {
-        const bool lds_items = c->lds_bytes <= kLdsSceneMax && c->variant != 3;
+        const bool lds_items = lds_staged(c);
         p.pull_batch = c->pull_batch ? c->pull_batch
                                      : (lds_items && p.group <= 2 ? (p.group == 1 ? 128 : 64) : (int)kPullBatch);
     }
@@ -3101,7 +3138,7 @@ static int enqueue_render(pt_ctx* c, int frame_first, int n_frames, int acc_firs
     // variants: 0 state-machine persistent (default), 1 one-lane-per-pixel tiles,
     // 2 while-while persistent, 3 = 0 with the scene forced to stay in global memory
     const int variant = c->variant == 4 ? 0 : c->variant;   // variant 4's fallback is variant 0
-    bool use_lds = (variant == 0 || variant == 2) && c->lds_bytes <= kLdsSceneMax;
+    bool use_lds = (variant == 0 && lds_staged(c)) || (variant == 2 && c->lds_bytes <= kLdsSceneSmall);
     if (variant != 1 && !wfP) HIPCHK(c, hipMemsetAsync(c->d_work, 0, sizeof(unsigned), c->stream));
     if (wfP) {
         HIPCHK(c, hipMemsetAsync(c->d_work, 0, 8 * sizeof(unsigned), c->stream));
@@ -3113,11 +3150,11 @@ static int enqueue_render(pt_ctx* c, int frame_first, int n_frames, int acc_firs
         while (p.wf_ring < wfP) p.wf_ring <<= 1;
         p.wf_err = c->d_work + 4;            // reset with the queue counter below
         // keysweep: LDS scenes 16 (+4% over 40), global-memory scenes 40 (+15% over 16)
-        p.wf_refill = c->wf_refill ? c->wf_refill : (c->lds_bytes <= kLdsSceneMax ? 16 : 40);
+        p.wf_refill = c->wf_refill ? c->wf_refill : (c->lds_bytes <= kLdsSceneSmall ? 16 : 40);
         p.wf_leaf_min = c->wf_leaf_min ? c->wf_leaf_min : 64;
         p.wf_shade_min = c->wf_shade_min ? c->wf_shade_min : 64;
         const size_t lds = (size_t)wf_scene_bytes(c) + 96 * (size_t)wfP + 3 * (size_t)p.wf_ring * 2 + 64;
-        const bool wl = c->lds_bytes <= kLdsSceneMax;      // LDS-staged scene (else global)
+        const bool wl = c->lds_bytes <= kLdsSceneSmall;    // LDS-staged scene (else global)
         const unsigned long long ids = (unsigned long long)c->n_tiles * 64ull *
                                        (unsigned long long)((n_frames + p.group - 1) / p.group);
         const int nt = wf_threads(c);
@@ -3147,7 +3184,10 @@ static int enqueue_render(pt_ctx* c, int frame_first, int n_frames, int acc_firs
         size_t lds = use_lds ? ((PT_WALK_SINKS && p.cons_walk) ? c->lds_bytes_sk : c->lds_bytes) : 0;
         unsigned tiles = (unsigned)(((p.W + 7) / 8) * ((c->rows_local + 7) / 8));
         unsigned items = tiles * (unsigned)((n_frames + p.group - 1) / p.group);   // 64-lane items
-        unsigned blocks = std::min<unsigned>(c->persist_blocks, std::max(1u, (items + 3) / 4));
+        const int nt = (variant == 0 && use_lds) ? lds_threads(c, lds) : 256;
+        const unsigned wpb = (unsigned)nt / 64u;                                    // waves per block
+        unsigned blocks = std::min<unsigned>(c->persist_blocks * 256u / (unsigned)nt,
+                                             std::max(1u, (items + wpb - 1) / wpb));
         dim3 grid(blocks);
 #define PT_LAUNCH(K, L, MW)                                                                                   \
     if (c->counting) hipLaunchKernelGGL((K<true, L, MW>), grid, dim3(256), L ? lds : 0, c->stream, p);        \
@@ -3173,7 +3213,15 @@ static int enqueue_render(pt_ctx* c, int frame_first, int n_frames, int acc_firs
     else if (p.rgb) hipLaunchKernelGGL((k_render_sm<false, L, 5, M, true>), grid, dim3(256), L ? lds : top_lds, c->stream, p); \
     else if (mw >= 6) hipLaunchKernelGGL((k_render_sm<false, L, 6, M, false>), grid, dim3(256), L ? lds : top_lds, c->stream, p); \
     else hipLaunchKernelGGL((k_render_sm<false, L, 5, M, false>), grid, dim3(256), L ? lds : top_lds, c->stream, p);
-        if (variant == 0 || variant == 3) {
+#define PT_LAUNCH_WIDE(NT)                                                                                    \
+    if (p.rgb) hipLaunchKernelGGL((k_render_sm<false, true, 7, false, true, false, NT>), grid, dim3(NT), lds, c->stream, p); \
+    else hipLaunchKernelGGL((k_render_sm<false, true, 7, false, false, false, NT>), grid, dim3(NT), lds, c->stream, p);
+        if (nt > 256) {           // lds_threads: LDS scene, variant 0, one ray per pixel, 7 waves
+            if (nt == 512) { PT_LAUNCH_WIDE(512) }
+            else if (nt == 768) { PT_LAUNCH_WIDE(768) }
+            else { PT_LAUNCH_WIDE(1024) }
+#undef PT_LAUNCH_WIDE
+        } else if (variant == 0 || variant == 3) {
             bool multi = p.rpp > 1;
             if (use_lds && multi) { PT_LAUNCH_SM(true, true) }
             else if (use_lds) { PT_LAUNCH_SM(true, false) }

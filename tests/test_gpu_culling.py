@@ -188,3 +188,20 @@ def test_sink_image_never_costs_a_workgroup(cornell_scene, tmp_path):
         assert np.array_equal(bits(pt.read_rgba32f()), bits(want))
     finally:
         pt.close()
+
+
+@pytest.mark.parametrize("target", [200, 380])
+def test_wide_workgroup_lds_scenes(tmp_path, target):
+    """Scenes past the 256-thread workgroups' LDS budget (48 KiB) are staged once per 768- or
+    1024-thread workgroup (lds_threads); culling on and off, the reference's image."""
+    import pt_scenes
+    sc = H.setupBuffers(*pt_scenes.write_scene("bunny", str(tmp_path), target_tris=target))
+    pt = H.PathTracer(16, 16, max_bounce=8)
+    try:
+        pt.upload(sc)
+        d = pt.diag()
+    finally:
+        pt.close()
+    assert 48 * 1024 < d["lds_bytes"] <= 152 * 1024, d
+    on = blocks_per_cu(d["lds_bytes_sinks"], 7) >= blocks_per_cu(d["lds_bytes"], 7)
+    check(sc, "%d-triangle wide-workgroup scene" % target, n_frames=3, expect_active=on)

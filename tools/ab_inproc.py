@@ -2,7 +2,7 @@
 ctypes handle through its own copy of pt_host), and their renders are interleaved round by
 round, so clock and thermal drift between processes does not enter the comparison.
 
-python tools/ab_inproc.py --libs base,cur --rounds 4 --spp 128 --chunk 128 [--scene bunny]
+python tools/ab_inproc.py --libs base,cur --rounds 4 --spp 128 --chunk 128 [--scene bunny [--tris 300]]
 ('cur' = build/libptrace.so, other names = build/libptrace_<name>.so from tools/ab_build.sh)
 """
 import argparse
@@ -35,12 +35,15 @@ def main():
     ap.add_argument("--spp", type=int, default=128)
     ap.add_argument("--chunk", type=int, default=128)
     ap.add_argument("--scene", default="cornell")
+    ap.add_argument("--tris", type=int, default=0, help="generator target_tris (bunny / sponza)")
     ap.add_argument("--width", type=int, default=1920)
     ap.add_argument("--height", type=int, default=1080)
     a = ap.parse_args()
     libs = a.libs.split(",")
     hosts = {l: load_host(l) for l in libs}
-    obj, mtl = pt_scenes.write_scene(a.scene, os.path.join(REPO, "scenes"))
+    kw = {"target_tris": a.tris} if a.tris else {}
+    obj, mtl = pt_scenes.write_scene(a.scene, os.path.join(REPO, "scenes", "%s_%d" % (a.scene, a.tris)) if a.tris
+                                     else os.path.join(REPO, "scenes"), **kw)
     pts, seg = {}, {}
     for l in libs:
         H = hosts[l]
