@@ -3213,13 +3213,15 @@ static int enqueue_render(pt_ctx* c, int frame_first, int n_frames, int acc_firs
     else if (p.rgb) hipLaunchKernelGGL((k_render_sm<false, L, 5, M, true>), grid, dim3(256), L ? lds : top_lds, c->stream, p); \
     else if (mw >= 6) hipLaunchKernelGGL((k_render_sm<false, L, 6, M, false>), grid, dim3(256), L ? lds : top_lds, c->stream, p); \
     else hipLaunchKernelGGL((k_render_sm<false, L, 5, M, false>), grid, dim3(256), L ? lds : top_lds, c->stream, p);
-#define PT_LAUNCH_WIDE(NT)                                                                                    \
-    if (p.rgb) hipLaunchKernelGGL((k_render_sm<false, true, 7, false, true, false, NT>), grid, dim3(NT), lds, c->stream, p); \
-    else hipLaunchKernelGGL((k_render_sm<false, true, 7, false, false, false, NT>), grid, dim3(NT), lds, c->stream, p);
-        if (nt > 256) {           // lds_threads: LDS scene, variant 0, one ray per pixel, 7 waves
-            if (nt == 512) { PT_LAUNCH_WIDE(512) }
-            else if (nt == 768) { PT_LAUNCH_WIDE(768) }
-            else { PT_LAUNCH_WIDE(1024) }
+#define PT_LAUNCH_WIDE(NT, MW)                                                                                \
+    if (p.rgb) hipLaunchKernelGGL((k_render_sm<false, true, MW, false, true, false, NT>), grid, dim3(NT), lds, c->stream, p); \
+    else hipLaunchKernelGGL((k_render_sm<false, true, MW, false, false, false, NT>), grid, dim3(NT), lds, c->stream, p);
+        // lds_threads: LDS scene, variant 0, one ray per pixel; the register budget of the
+        // waves that are resident (6, 6, 4 per SIMD), not of 7
+        if (nt > 256) {
+            if (nt == 512) { PT_LAUNCH_WIDE(512, 6) }
+            else if (nt == 768) { PT_LAUNCH_WIDE(768, 6) }
+            else { PT_LAUNCH_WIDE(1024, 4) }
 #undef PT_LAUNCH_WIDE
         } else if (variant == 0 || variant == 3) {
             bool multi = p.rpp > 1;
