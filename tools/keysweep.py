@@ -18,6 +18,7 @@ import pt_scenes  # noqa: E402
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--scene", default="cornell")
+    ap.add_argument("--tris", type=int, default=0, help="generator target_tris (bunny / sponza)")
     ap.add_argument("--spp", type=int, default=64)
     ap.add_argument("--chunk", type=int, default=None)
     ap.add_argument("--width", type=int, default=1920)
@@ -30,7 +31,9 @@ def main():
     a = ap.parse_args()
     chunk = a.chunk or a.spp
     cfgs = [[tuple(int(x) for x in kv.split("=")) for kv in c.split(",") if kv] for c in a.configs.split(";")]
-    sb = pt_host.setupBuffers(*pt_scenes.write_scene(a.scene, os.path.join(REPO, "scenes")))
+    kw = {"target_tris": a.tris} if a.tris else {}
+    sdir = os.path.join(REPO, "scenes", "%s_%d" % (a.scene, a.tris)) if a.tris else os.path.join(REPO, "scenes")
+    sb = pt_host.setupBuffers(*pt_scenes.write_scene(a.scene, sdir, **kw))
     pt = pt_host.PathTracer(a.width, a.height, max_bounce=a.bounces, world=a.world)
     pt.set_kernel(a.variant)
     pt.upload(sb)
