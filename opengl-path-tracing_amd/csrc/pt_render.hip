@@ -2349,6 +2349,7 @@ struct pt_ctx {
     float cons_m[3] = {0, 0, 0};   // KParams::cons_m
     size_t lds_bytes = 0;
     unsigned persist_blocks = 2048;
+    int order_skip = 0;             // short launches since the last tile-order sort
     // 0 = automatic: 52/44 when the scene is staged in LDS (best on C2 since the octant walk),
     // 20/24 when the walk reads global memory (re-swept after the leaf compaction: +2% on
     // the C3 stand-in, +3% on C4 over 16/32; leaf 20 re-swept in round 2: C3 +1.3%, C4 +0.6%
@@ -2951,6 +2952,7 @@ static int plan_group(const pt_ctx* c, int n_frames) {
 // per frame in long launches.  In automatic mode such launches use the split path and its
 // batched reservations; pt_set_tuning key 5 >= n_frames still forces register mode.
 constexpr int kShortLaunch = 16;
+constexpr int kOrderEvery = 8;    // short launches per tile-order sort (enqueue_render)
 static bool split_mode(const pt_ctx* c, int n_frames, int group) {
     if (group < n_frames) return true;
     return c->group_force == 0 && (c->variant == 0 || c->variant == 3) && n_frames <= kShortLaunch;
@@ -3242,9 +3244,16 @@ static int enqueue_render(pt_ctx* c, int frame_first, int n_frames, int acc_firs
             hipLaunchKernelGGL(k_accum_frames, dim3((unsigned)((px + 255) / 256)), dim3(256), 0, c->stream, p);
         }
     }
-    if (p.tile_cost && c->n_tiles > 1)
+    // The queue order is recomputed from the accumulated tile costs after every long launch,
+    // but only after every kOrderEvery-th short one: a one-frame 1080p launch gains about
+    // what the 32-us single-workgroup sort costs (adaptive off: +0.5%), so the costs of 8
+    // launches are pooled into one sort.  Captured graphs (frame_dev) sort every replay.
+    if (p.tile_cost && c->n_tiles > 1 &&
+        (frame_dev || n_frames > kShortLaunch || ++c->order_skip >= kOrderEvery)) {
+        c->order_skip = 0;
         hipLaunchKernelGGL(k_tile_order, dim3(1), dim3(1024), 0, c->stream, c->d_tile_cost, c->d_tile_perm,
                            c->n_tiles, c->tiles_x);
+    }
     HIPCHK(c, hipGetLastError());
     return PT_OK;
 }
