@@ -2350,6 +2350,7 @@ struct pt_ctx {
     size_t lds_bytes = 0;
     unsigned persist_blocks = 2048;
     int order_skip = 0;             // short launches since the last tile-order sort
+    bool order_sorted = false;      // a sort ran since the scene upload
     // 0 = automatic: 52/44 when the scene is staged in LDS (best on C2 since the octant walk),
     // 20/24 when the walk reads global memory (re-swept after the leaf compaction: +2% on
     // the C3 stand-in, +3% on C4 over 16/32; leaf 20 re-swept in round 2: C3 +1.3%, C4 +0.6%
@@ -2773,6 +2774,8 @@ int pt_upload_scene(pt_ctx* c, const float* tris, int n_tris, const float* bvh, 
         if (!(nd[0] <= nd[4] && nd[1] <= nd[5] && nd[2] <= nd[6])) c->scene_fast = 0;
     }
     c->walk_nested = nested;
+    c->order_sorted = false;      // the next sort pools the new scene's first short launches
+    c->order_skip = 0;
     if (n_nodes > 0) {   // every box lies in the root box (nested): M_i bounds each |coordinate|
         for (int q = 0; q < 3; q++) {
             const double m = std::max(std::fabs((double)bvh[q]), std::fabs((double)bvh[4 + q]));
@@ -2899,6 +2902,8 @@ int pt_set_tuning(pt_ctx* c, int key, int value) {
     }
     else if (key == 2) {
         c->adaptive = value != 0;
+        c->order_sorted = false;
+        c->order_skip = 0;
         if (!c->adaptive && c->n_tiles > 0) {       // back to raster order
             std::vector<unsigned> ident(c->n_tiles);
             for (int i = 0; i < c->n_tiles; i++) ident[i] = pack_tile(c, (unsigned)i);
@@ -2952,7 +2957,11 @@ static int plan_group(const pt_ctx* c, int n_frames) {
 // per frame in long launches.  In automatic mode such launches use the split path and its
 // batched reservations; pt_set_tuning key 5 >= n_frames still forces register mode.
 constexpr int kShortLaunch = 16;
-constexpr int kOrderEvery = 8;    // short launches per tile-order sort (enqueue_render)
+#ifndef PT_ORDER_EVERY
+#define PT_ORDER_EVERY 64
+#endif
+constexpr int kOrderEvery = PT_ORDER_EVERY;   // short launches per tile-order sort (enqueue_render)
+constexpr int kOrderFirst = 8;                // ... and before the first sort after an upload
 static bool split_mode(const pt_ctx* c, int n_frames, int group) {
     if (group < n_frames) return true;
     return c->group_force == 0 && (c->variant == 0 || c->variant == 3) && n_frames <= kShortLaunch;
@@ -3245,12 +3254,16 @@ static int enqueue_render(pt_ctx* c, int frame_first, int n_frames, int acc_firs
         }
     }
     // The queue order is recomputed from the accumulated tile costs after every long launch,
-    // but only after every kOrderEvery-th short one: a one-frame 1080p launch gains about
-    // what the 32-us single-workgroup sort costs (adaptive off: +0.5%), so the costs of 8
-    // launches are pooled into one sort.  Captured graphs (frame_dev) sort every replay.
+    // but only after every kOrderEvery-th short one (the first time after kOrderFirst): a
+    // sort after each one-frame 1080p launch cost more than the order gained (adaptive off:
+    // +0.5%), while a sorted order, even one 64 frames old, keeps most of the gain
+    // (same-process A/B of one-frame launches, against sorting every launch: every 4th
+    // +6%, 8th +8.4%, 16th +9.8%, 64th +10.7%).  Captured graphs (frame_dev) sort every replay.
     if (p.tile_cost && c->n_tiles > 1 &&
-        (frame_dev || n_frames > kShortLaunch || ++c->order_skip >= kOrderEvery)) {
+        (frame_dev || n_frames > kShortLaunch ||
+         ++c->order_skip >= (c->order_sorted ? kOrderEvery : kOrderFirst))) {
         c->order_skip = 0;
+        c->order_sorted = true;
         hipLaunchKernelGGL(k_tile_order, dim3(1), dim3(1024), 0, c->stream, c->d_tile_cost, c->d_tile_perm,
                            c->n_tiles, c->tiles_x);
     }
