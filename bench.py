@@ -30,6 +30,7 @@ sys.path.insert(0, PKG)
 
 METRIC = "Mrays/sec + ms/frame @1920×1080, 8 bounces, 1/2/4/8 MI355X"
 HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
+N_SIMD = 1024           # 256 CUs x 4 SIMDs; a wave64 VALU instruction holds a SIMD-32 for 2 cycles
 
 # scene, W, H, spp, bounces, frames per launch, graph launches/replay
 CONFIGS = {
@@ -48,6 +49,32 @@ def algorithmic_bytes(cnt, pixels, first_launch_plain):
     return b + pixels * (16 if first_launch_plain else 32)
 
 
+def cpu_share():
+    """-> (threads, description): the CPUs this process may run on -- its affinity mask, capped
+    by a cgroup v2 cpu.max quota when one is set (os.cpu_count() counts the whole machine)."""
+    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    desc = "affinity %d" % n
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()
+        if q != "max":
+            lim = max(1, int(int(q) // int(per)))
+            desc += ", cgroup quota %s/%s = %d" % (q, per, lim)
+            n = min(n, lim)
+    except (OSError, ValueError):
+        pass
+    return n, desc
+
+
+def cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -60,8 +87,9 @@ def main():
     ap.add_argument("--height", type=int, default=None)
     ap.add_argument("--bounces", type=int, default=None)
     ap.add_argument("--variant", type=int, default=0)
-    ap.add_argument("--cpu-spp", type=int, default=1, help="spp of the bounded CPU-baseline sample")
-    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--cpu-spp", type=int, default=2, help="spp of the bounded CPU-baseline sample")
+    ap.add_argument("--cpu-threads", type=int, default=0, help="0 = every CPU this process may use")
+    ap.add_argument("--no-cold", action="store_true", help="skip the cold first-render measurement")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="nccl = RCCL over xGMI (default); gloo = CPU rehearsal of the N>1 path")
@@ -116,6 +144,30 @@ def main():
     obj = os.path.join(scene_dir, "%sobj.txt" % scene)
     mtl = os.path.join(scene_dir, "%smtl.txt" % scene)
     sb = pt_host.setupBuffers(obj, mtl)
+    cold_ms = None
+    if not args.no_cold and graph_launches == 0:
+        # cold first render: a fresh context right after pt_upload_scene (raster tile order
+        # until the probe launch's costs are sorted), after a tiny render on a throw-away
+        # context has loaded the code object -- what one render of a new scene costs
+        warm = pt_host.PathTracer(64, 32, max_bounce=bounces, device=device)
+        warm.upload(sb)
+        warm.render(1, 2, 0)
+        warm.close()
+        cold = pt_host.PathTracer(W, H, max_bounce=bounces, display_mode=1, device=device, rank=rank, world=world)
+        cold.set_kernel(args.variant)
+        cold.upload(sb)
+        barrier()
+        tc = time.perf_counter()
+        for f0 in range(1, spp + 1, chunk):
+            cold.render_async(f0, min(chunk, spp - (f0 - 1)), 0 if f0 == 1 else 1)
+        cold.sync()
+        cold_ms = (time.perf_counter() - tc) * 1e3
+        cold.close()
+        if distributed:
+            t = torch.tensor([cold_ms], dtype=torch.float64,
+                             device="cuda" if args.dist_backend == "nccl" else "cpu")
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            cold_ms = float(t.item())
     pt = pt_host.PathTracer(W, H, max_bounce=bounces, display_mode=1, device=device, rank=rank, world=world)
     pt.set_kernel(args.variant)
     pt.upload(sb)
@@ -193,35 +245,66 @@ def main():
     bytes_per_launch = alg_bytes / len(launches)       # this rank's launches
     achieved = bytes_per_launch / (avg_launch_ms * 1e-3) / 1e9
 
-    traffic = None
-    valu = None
+    # Roofline.  The scene is LDS/L2-resident, so HBM does not bound the kernel (the algorithmic
+    # bytes exceed the HBM peak); the bound that binds is VALU issue.  Its per-launch
+    # instruction count and held clock come from a PMC pass of the same build and workload
+    # (tools/gpu_pmc.sh -> tools/pmc_traffic.py -> profiles/traffic_latest.json):
+    #   achieved = SQ_INSTS_VALU per launch / the live launch time (HIP events, this run)
+    #   peak     = 1024 SIMDs x held clock / 2 cycles per wave64 VALU instruction
+    #   busy_frac_pmc = SQ_INSTS_VALU x 2 / (1024 x GRBM_GUI_ACTIVE / 8), all from the PMC pass
+    pmc = None
     try:
         with open(args.traffic_json) as fh:
             tj = json.load(fh)
         if (tj.get("width"), tj.get("height"), tj.get("chunk"), tj.get("scene")) == (W, H, chunk, scene) \
                 and world == 1:
-            traffic = tj.get("hbm_bytes_per_launch")
-            if tj.get("valu_busy_frac") is not None:
-                valu = {"busy_frac": round(tj["valu_busy_frac"], 4),
-                        "active_lanes_per_instr": round(tj.get("valu_active_lanes_per_instr", 0.0), 2),
-                        "source": "PMC (tools/gpu_pmc.sh -> tools/pmc_traffic.py): SQ_INSTS_VALU x 2 cycles "
-                                  "/ (1024 SIMDs x GRBM_GUI_ACTIVE/8) -- the bound that actually binds"}
+            pmc = tj
     except (OSError, ValueError):
         pass
+    hbm = {"algorithmic_gbs": round(achieved, 1), "algorithmic_frac": round(achieved / HBM_PEAK_GBS, 4),
+           "algorithmic_bytes_per_launch": int(bytes_per_launch), "peak": HBM_PEAK_GBS, "unit": "GB/s"}
+    roofline = {"bound": "valu", "achieved": None, "peak": None, "unit": "G wave-VALU instr/s", "frac": None,
+                "traffic": None, "avg_launch_ms": round(avg_launch_ms, 3), "n_launches": n_launch}
+    if pmc is not None and pmc.get("valu_instr_per_launch"):
+        cnt = pmc["counters_per_launch"]
+        vi = pmc["valu_instr_per_launch"]
+        clk = pmc["clock_ghz"]
+        roofline.update(achieved=round(vi / (avg_launch_ms * 1e-3) / 1e9, 2), peak=round(N_SIMD * clk / 2.0, 2))
+        roofline["frac"] = round(roofline["achieved"] / roofline["peak"], 4)
+        roofline["busy_frac_pmc"] = round(pmc["valu_busy_frac"], 4)
+        roofline["clock_ghz_pmc"] = round(clk, 3)
+        roofline["valu_instr_per_launch"] = vi
+        roofline["valu_instr_per_segment"] = round(vi / (seg_all / len(launches)), 2)
+        roofline["active_lanes_per_valu"] = round(pmc.get("valu_active_lanes_per_instr", 0.0), 2)
+        if pmc.get("hbm_bytes_per_launch"):
+            tb = pmc["hbm_bytes_per_launch"]
+            roofline["traffic"] = int(tb)
+            hbm.update(traffic_bytes_per_launch=int(tb), measured_gbs=round(tb / (avg_launch_ms * 1e-3) / 1e9, 1),
+                       measured_frac=round(tb / (avg_launch_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+                       traffic_over_algorithmic=round(tb / bytes_per_launch, 2))
+        roofline["source"] = pmc.get("source", "profiles/traffic_latest.json")
+    roofline["hbm"] = hbm
+    roofline["basis"] = ("VALU issue: achieved = PMC SQ_INSTS_VALU per launch / live avg launch time (HIP events on "
+                         "the render stream); peak = 1024 SIMDs x PMC-held clock / 2; HBM kept as a secondary "
+                         "field (algorithmic bytes, SURVEY.md §8(d), and PMC-measured traffic)")
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         sys.path.insert(0, os.path.join(REPO, "tests"))
         import oracle_lib
-        threads = min(args.cpu_threads, os.cpu_count() or 1)
+        threads, share = cpu_share()
+        if args.cpu_threads:
+            threads = args.cpu_threads
         t1 = time.perf_counter()
         _, ccnt = oracle_lib.render(sb, W, H, max_bounce=bounces, n_frames=args.cpu_spp, threads=threads,
                                     counters=True)
         cdt = time.perf_counter() - t1
         cpu = {"value": round(float(ccnt[0]) / cdt / 1e6, 3), "unit": "Mrays/s", "cores": threads, "kind": "port",
-               "sample": "CPU restatement of computeShader.c semantics (oracle/pt_oracle.cpp, -O3, %d threads), "
-                         "same scene/camera/bounces at %dx%d, frames 1..%d (%d segments, %.2f s); "
-                         "ms/frame = %.1f" % (threads, W, H, args.cpu_spp, int(ccnt[0]), cdt, cdt * 1e3 / args.cpu_spp)}
+               "cpu_model": cpu_model(), "host_cpus": os.cpu_count(), "cpu_share": share,
+               "sample": "CPU restatement of computeShader.c semantics (oracle/pt_oracle.cpp, -O3, %d threads = this "
+                         "process's CPU share), same scene/camera/bounces at %dx%d, frames 1..%d (%d segments, "
+                         "%.2f s); ms/frame = %.1f" % (threads, W, H, args.cpu_spp, int(ccnt[0]), cdt,
+                                                        cdt * 1e3 / args.cpu_spp)}
 
     if rank == 0:
         line = {
@@ -238,13 +321,9 @@ def main():
                                        % (world, "RCCL" if args.dist_backend == "nccl" else "gloo"))
                        if world > 1 else "single GPU"},
             "ms_per_frame": round(ms_per_step / spp, 4),
+            "cold_ms_per_step": None if cold_ms is None else round(cold_ms, 3),
             "segments_per_step": int(seg_all),
-            "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-                         "basis": "algorithmic bytes (SURVEY.md §8(d)) per launch / avg launch time (HIP events "
-                                  "on the render stream, %d launches); the scene is cache/LDS-resident so frac "
-                                  "can exceed 1; traffic = PMC HBM bytes per launch (profiles/)" % n_launch,
-                         "avg_launch_ms": round(avg_launch_ms, 3), "valu": valu},
+            "roofline": roofline,
             "cpu_baseline": cpu,
         }
         print(json.dumps(line), flush=True)

@@ -129,9 +129,8 @@ int pt_stats_ex(pt_ctx* ctx, unsigned long long out[16]);
  * launches since the last reset; reset != 0 clears both after reading. */
 int pt_timing(pt_ctx* ctx, double* total_kernel_ms, int* n_launches, int reset);
 
-/* Kernel variant selection (0 = default/fastest); see DESIGN.md §5 for the list.
- * 4 = wavefront queues (experimental): raysPerPixel 1, no counting, materials + spheres
- * within 4 KiB for global-memory scenes; otherwise it runs variant 0. */
+/* Kernel variant selection: 0 = the state-machine kernel (default), 3 = the same kernel with
+ * the scene kept in global memory even when it would fit LDS (A/B of the LDS staging). */
 int pt_set_kernel(pt_ctx* ctx, int variant);
 /* Scheduling knobs of the state-machine kernel:
  * key 0 = run the leaf phase once this many lanes wait at leaves (1..64, 0 = auto),
@@ -156,11 +155,6 @@ int pt_set_kernel(pt_ctx* ctx, int variant);
  *         A render whose per-frame colours (12 B per pixel-frame) exceed it -- or whose
  *         32-bit work-queue ids would overflow -- runs as back-to-back launches, the first
  *         with the caller's accumulate flag and the rest accumulating: the same image.
- * keys 10-14 = variant 4 (wavefront queues): 10 path slots per workgroup (64..1536, 0 = as
- *         many as fit beside the scene), 11 walkers below which a wave refills (0 = 16 for
- *         LDS-staged scenes, 40 for global-memory scenes),
- *         12 / 13 leaf / shade batch minimum (1..64, 0 = 64), 14 threads per workgroup
- *         (512, 768, 896, 1024; 0 = 1024).
  * key 15 = culling walk (0 = automatic, 1 = off).  When the uploaded tree is a full binary
  *         tree threaded in preorder whose internal boxes contain their children's, the
  *         LDS-staged walk tests nodes with a cheaper conservative slab test and re-tests a

@@ -84,10 +84,6 @@ struct KParams {
     // a leaf): a ray starting inside the root box hits it, so the walk may start at the child
     float root_box[6];
     int root_child;
-    // variant 4 (wavefront kernel): path slots per workgroup, the walker count at which a
-    // wave stops walking to refill, and the queue depths that start a leaf / shade batch
-    int wf_paths, wf_ring, wf_refill, wf_leaf_min, wf_shade_min;
-    unsigned* wf_err;              // watchdog trips of the wavefront kernel (must stay 0)
     int shade_lds;                 // global-memory scene: materials + spheres staged in LDS too
     int cons_walk;                 // LDS scene: the culling walk (slab_oct_cons, exact leaf re-test)
     float cons_m[3];               // ... 2^-19 * the scene's largest |coordinate| per axis, rounded up
@@ -148,24 +144,6 @@ __device__ __forceinline__ bool slab(float4 A, float4 B, f3 o, f3 d, float cur_t
     return !(tmin > cur_t);
 }
 
-// hit_triangle (computeShader.c:274-307) with the per-triangle normal and plane offset
-// precomputed (same ops, same bits).  Returns -1 for a miss.  `tbest` cull: a hit at
-// t >= tbest can never be selected by the leaf's 2-way choice (:411-428), and a culled
-// value behaves like a miss in that choice, so culling before the edge tests is exact.
-__device__ __forceinline__ float tri_hit(const float4* T, f3 o, f3 d, float tbest, f3& n) {
-    float4 q0 = T[0], q1 = T[1], q2 = T[2], q3 = T[3];
-    n = mk(q0.x, q0.y, q0.z);
-    float t = -(pt::dot(n, o) + q0.w) / pt::dot(n, d);
-    if (t < 0.0f) return -1.0f;
-    if (!(t < tbest)) return -1.0f;
-    f3 v0 = mk(q1.x, q1.y, q1.z), v1 = mk(q2.x, q2.y, q2.z), v2 = mk(q3.x, q3.y, q3.z);
-    f3 p = o + d * t;
-    if (!(pt::dot(n, pt::cross(v1 - v0, p - v0)) > 0.0f)) return -1.0f;
-    if (!(pt::dot(n, pt::cross(v2 - v1, p - v1)) > 0.0f)) return -1.0f;
-    if (!(pt::dot(n, pt::cross(v0 - v2, p - v2)) > 0.0f)) return -1.0f;
-    return t;
-}
-
 // A ray with a NaN component in o or d can never hit: every triangle distance
 // -(dot(n,o)+d0)/dot(n,d) and every sphere root is NaN, and NaN fails the `t < tbest` /
 // `ht > 0.0001` acceptance tests (:297, :378, :411-428).  Its walk still visits up to every
@@ -199,143 +177,6 @@ __device__ __forceinline__ float tri_mt(float4 q0, float4 q1, float4 q2, f3 o, f
     ok = ok && t > EPS;
     return ok ? t : -1.0f;
 }
-__device__ __forceinline__ float tri_test(int flags, const float4* T, f3 o, f3 d, float tbest, f3& n) {
-    if (flags & PT_FLAG_MOLLER_TRUMBORE) {
-        n = mk(T[0].x, T[0].y, T[0].z);
-        return tri_mt(T[1], T[2], T[3], o, d);
-    }
-    return tri_hit(T, o, d, tbest, n);
-}
-
-// calculateRayCollision (computeShader.c:367-432)
-template <bool COUNT>
-__device__ __forceinline__ bool collide(const KParams& p, f3 o, f3 d, f3& normal, f3& hitp,
-                                        int& mat, Cnt& c) {
-    float t = __builtin_huge_valf();
-    bool hit = false;
-    if (!(p.flags & PT_FLAG_NO_SPHERES)) {
-        for (int si = 0; si < p.sc.n_spheres; si++) {
-            float4 s0 = p.sc.spheres[2 * si];
-            f3 cc = mk(s0.x, s0.y, s0.z);
-            f3 oc = o - cc;
-            float a = pt::dot(d, d);
-            float half_b = pt::dot(oc, d);
-            float cq = pt::dot(oc, oc) - s0.w;
-            float disc = half_b * half_b - a * cq;
-            float ht = disc < 0.0f ? -1.0f : (-half_b - pt::fsqrt(disc)) / a;
-            if (COUNT) c.sph++;
-            if (ht > 0.0001f && ht < t) {
-                f3 pn = pt::normalize((o + d * ht) - cc);
-                if (pt::dot(pn, d) > 0.0f) pn = pn * -1.0f;
-                hit = true;
-                t = ht;
-                normal = pn;
-                hitp = o + d * ht;
-                mat = __float_as_int(p.sc.spheres[2 * si + 1].x);
-            }
-        }
-    }
-    if ((p.flags & PT_FLAG_NO_TRIANGLES) || p.sc.n_nodes <= 0) return hit;
-    if (!COUNT && ray_has_nan(o, d)) return hit;
-    int bi = 0;
-    for (int steps = 0; bi > -1 && steps < p.sc.n_nodes; steps++) {
-        float4 lo = p.sc.nodes[2 * bi], hi = p.sc.nodes[2 * bi + 1];
-        int a = __float_as_int(hi.z), b = __float_as_int(hi.w);
-        bool hb = slab(lo, hi, o, d, t);
-        if (COUNT) c.nodes++;
-        int next = (hb && a >= 0) ? a : b;
-        if (hb && a < 0) {
-            if (COUNT) c.tri += 2;
-            int code = ~a;
-            const float4* T0 = p.sc.tris + 8 * (code >> 2);
-            f3 n0, n1;
-            float h1 = tri_test(p.flags, T0, o, d, t, n0);
-            float h2 = (code & 1) ? h1 : tri_test(p.flags, T0 + 4, o, d, t, n1);
-            if (code & 1) n1 = n0;
-            if (h1 > 0.0001f && h1 < t && (h1 < h2 || h2 < 0.0001f)) {
-                if (pt::dot(n0, d) > 0.0f) n0 = n0 * -1.0f;
-                hit = true;
-                t = h1;
-                normal = n0;
-                hitp = o + d * h1;
-                mat = __float_as_int(T0[2].w);
-            } else if (h2 > 0.0001f && h2 < t) {
-                if (pt::dot(n1, d) > 0.0f) n1 = n1 * -1.0f;
-                hit = true;
-                t = h2;
-                normal = n1;
-                hitp = o + d * h2;
-                mat = __float_as_int(T0[(code & 1) ? 2 : 6].w);
-            }
-        }
-        bi = next;
-    }
-    return hit;
-}
-
-// Trace (computeShader.c:434-501)
-template <bool COUNT>
-__device__ f3 trace(const KParams& p, f3 o, f3 d, uint32_t& state, Cnt& c) {
-    f3 incoming = mk(0, 0, 0), ray_color = mk(1, 1, 1);
-    f3 normal = mk(0, 0, 0), hitp = mk(0, 0, 0);
-    int mat = 0;
-    for (int i = 0; i <= p.max_bounce; i++) {
-        bool hit = collide<COUNT>(p, o, d, normal, hitp, mat, c);
-        if (COUNT) { c.seg++; if (hit) c.hits++; }
-        if (hit && pt::length(ray_color) > 0.01f) {
-            if (p.mode == 2) return (normal + mk(1, 1, 1)) * 0.5f;
-            if (p.mode == 4) {
-                float s = pt::length(hitp - o);
-                float dist = 1.0f - pt::fsqrt(s + 1.0f) / (s + 1.0f);
-                float q = dist * dist;
-                return mk(q, q, q);
-            }
-            o = hitp;
-            f3 diffuse = pt::normalize(normal + pt::random_unit_vector(state));
-            float k = 2.0f * pt::dot(normal, d);
-            f3 specular = pt::normalize(d - normal * k);
-            float4 m0 = p.sc.mats[3 * mat], m1 = p.sc.mats[3 * mat + 1], m2 = p.sc.mats[3 * mat + 2];
-            if (p.mode == 3) return mk(m0.x, m0.y, m0.z);
-            float is_spec = (m1.w > pt::random01(state)) ? 1.0f : 0.0f;
-            d = pt::mix(diffuse, specular, m0.w * is_spec);
-            incoming = incoming + mk(m1.x, m1.y, m1.z) * ray_color;
-            ray_color = ray_color * pt::mix(mk(m0.x, m0.y, m0.z), mk(m2.x, m2.y, m2.z), is_spec);
-        } else {
-            f3 env = mk(0, 0, 0);
-            if (!(p.flags & PT_FLAG_NO_SKY)) {
-                f3 dir = pt::normalize(d);
-                float tt = 0.5f * (dir.z + 1.0f);
-                float omt = 1.0f - tt;
-                env = mk(omt * 1.0f + tt * 0.5f, omt * 1.0f + tt * 0.7f, omt * 1.0f + tt * 1.0f);
-            }
-            incoming = incoming + env * ray_color;
-            break;
-        }
-    }
-    return incoming;
-}
-
-// main (computeShader.c:505-546): one sample of pixel (x, y) at `frame`.
-template <bool COUNT>
-__device__ __forceinline__ f3 sample_pixel(const KParams& p, int x, int y, int frame, Cnt& c) {
-    uint32_t state = pt::seed(x, y, frame);
-    f3 pos = mk(p.cam[0], p.cam[1], p.cam[2]), fwd = mk(p.cam[3], p.cam[4], p.cam[5]);
-    f3 right = mk(p.cam[6], p.cam[7], p.cam[8]), up = mk(p.cam[9], p.cam[10], p.cam[11]);
-    f3 pixel = mk(0, 0, 0);
-    for (int r = 0; r < p.rpp; r++) {
-        float ax = 0.0f, ay = 0.0f;
-        if (!(p.flags & PT_FLAG_NO_AA)) {
-            ax = pt::random01(state);
-            ay = pt::random01(state);
-        }
-        float u = ((float)x + ax) / (float)p.W - 0.5f;
-        float v = ((float)y + ay) / (float)p.H - 0.5f;
-        f3 d = pt::normalize((fwd + right * u) + up * v);
-        pixel = pixel + trace<COUNT>(p, pos, d, state, c);
-    }
-    return pixel / (float)p.rpp;
-}
-
 // :548-551 running mean, per component, no contraction.
 __device__ __forceinline__ float4 accumulate(float4 prev, f3 rgb, int frame, bool acc) {
     if (!acc) return make_float4(rgb.x, rgb.y, rgb.z, 1.0f);
@@ -371,40 +212,14 @@ __device__ __forceinline__ void flush_counters(const KParams& p, const Cnt& c) {
     }
 }
 
-// Variant 0: one lane per pixel, all n_frames fused in registers (one accumulator
-// read + write per launch), 16x16-pixel workgroups of four 8x8 wave tiles.
-template <bool COUNT>
-__global__ __launch_bounds__(256) void k_render_tiled(KParams p) {
-    resolve_frames(p);
-    int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    int lx = blockIdx.x * 16 + (wave & 1) * 8 + (lane & 7);
-    int lrow = blockIdx.y * 16 + (wave >> 1) * 8 + (lane >> 3);
-    Cnt c = {0, 0, 0, 0, 0};
-    int y = p.row0 + lrow * p.row_stride;
-    bool active = lx < p.W && lrow < p.rows_local && lx < p.x_limit && y < p.y_limit;
-    if (active) {
-        size_t idx = (size_t)lrow * p.W + lx;
-        float4 acc = p.acc_first ? p.accum[idx] : make_float4(0, 0, 0, 0);
-        for (int k = 0; k < p.n_frames; k++) {
-            int f = p.frame_first + k;
-            f3 rgb = sample_pixel<COUNT>(p, lx, y, f, c);
-            acc = accumulate(acc, rgb, f, k > 0 || p.acc_first == 1);
-        }
-        p.accum[idx] = acc;
-    }
-    flush_counters<COUNT>(p, c);
-}
-
 // =====================================================================================
-// Variant 0 (default): persistent wavefront kernel with path regeneration.
+// The render kernel: a persistent state-machine kernel with path regeneration.
 //
-// * Work = (pixel, all n_frames of this launch); lanes pull pixels from a device queue
-//   with one wave-aggregated atomic (ballot + popcount + shfl), 8x8-pixel tiles in queue
-//   order so a wave starts on a coherent tile.
-// * Every loop iteration runs ONE segment (calculateRayCollision + shading) for every
-//   busy lane; a lane whose path ended regenerates the next frame's camera ray in the
-//   next iteration instead of idling until the wave's longest path ends.  The frames of a
-//   pixel stay in order in one lane, so the running mean is bit-identical.
+// * Work items are (pixel, group of consecutive frames); lanes pull them from a device queue
+//   with wave-aggregated atomics, 8x8-pixel tiles in queue order so a wave starts on a
+//   coherent tile.  A lane whose path ended regenerates the next camera ray instead of
+//   idling until the wave's longest path ends.  A pixel's frames stay in order, so the
+//   running mean is bit-identical.
 // * Slab test in exact-reciprocal form: q = RN((b-o)/d) computed as q0 = (b-o)*rd,
 //   q = fma(fma(-q0, d, b-o), rd, q0) with rd = RN(1/d) per ray (Markstein's theorem:
 //   correctly rounded when no under/overflow).  The guard that makes that hold is checked
@@ -583,112 +398,6 @@ __device__ __forceinline__ int oct_base(f3 d, int img_bytes) {
     return (int)o * img_bytes;
 }
 
-template <bool COUNT>
-__device__ __forceinline__ bool collide_v(const SceneView& S, int n_nodes, int n_spheres, int flags,
-                                          f3 o, f3 d, bool fast, f3 rd, f3& normal, f3& hitp, int& mat,
-                                          Cnt& c) {
-    float t = __builtin_huge_valf();
-    bool hit = false;
-    if (!(flags & PT_FLAG_NO_SPHERES)) {
-        for (int si = 0; si < n_spheres; si++) {
-            float4 s0 = S.spheres[2 * si];
-            f3 cc = mk(s0.x, s0.y, s0.z);
-            f3 oc = o - cc;
-            float a = pt::dot(d, d);
-            float half_b = pt::dot(oc, d);
-            float cq = pt::dot(oc, oc) - s0.w;
-            float disc = half_b * half_b - a * cq;
-            float ht = disc < 0.0f ? -1.0f : (-half_b - pt::fsqrt(disc)) / a;
-            if (COUNT) c.sph++;
-            if (ht > 0.0001f && ht < t) {
-                f3 pn = pt::normalize((o + d * ht) - cc);
-                if (pt::dot(pn, d) > 0.0f) pn = pn * -1.0f;
-                hit = true;
-                t = ht;
-                normal = pn;
-                hitp = o + d * ht;
-                mat = __float_as_int(S.spheres[2 * si + 1].x);
-            }
-        }
-    }
-    if ((flags & PT_FLAG_NO_TRIANGLES) || n_nodes <= 0) return hit;
-    if (!COUNT && ray_has_nan(o, d)) return hit;
-    int bi = 0;
-    for (int steps = 0; bi > -1 && steps < n_nodes; steps++) {
-        float4 lo = S.nodes[2 * bi], hi = S.nodes[2 * bi + 1];
-        int a = __float_as_int(hi.z), b = __float_as_int(hi.w);
-        bool hb;
-        if (fast) hb = slab_fast(lo, hi, o, d, rd, t);
-        else hb = slab(lo, hi, o, d, t);
-        if (COUNT) c.nodes++;
-        int next = (hb && a >= 0) ? a : b;
-        if (hb && a < 0) {
-            if (COUNT) c.tri += 2;
-            int code = ~a;
-            const float4* T0 = S.tris + 8 * (code >> 2);
-            f3 n0, n1;
-            float h1 = tri_test(flags, T0, o, d, t, n0);
-            float h2 = h1;
-            n1 = n0;
-            if (!(code & 1)) h2 = tri_test(flags, T0 + 4, o, d, t, n1);
-            if (h1 > 0.0001f && h1 < t && (h1 < h2 || h2 < 0.0001f)) {
-                if (pt::dot(n0, d) > 0.0f) n0 = n0 * -1.0f;
-                hit = true;
-                t = h1;
-                normal = n0;
-                hitp = o + d * h1;
-                mat = __float_as_int(T0[2].w);
-            } else if (h2 > 0.0001f && h2 < t) {
-                if (pt::dot(n1, d) > 0.0f) n1 = n1 * -1.0f;
-                hit = true;
-                t = h2;
-                normal = n1;
-                hitp = o + d * h2;
-                mat = __float_as_int(T0[(code & 1) ? 2 : 6].w);
-            }
-        }
-        bi = next;
-    }
-    return hit;
-}
-
-// hit_triangle without early exits: every lane evaluates the full test and the verdict is
-// a select, so a wave does the test once instead of once per divergent exit path.
-// Same operations, same bits as tri_hit().
-__device__ __forceinline__ float tri_hit_bf(const float4* T, f3 o, f3 d, float tbest, f3& n) {
-    float4 q0 = T[0], q1 = T[1], q2 = T[2], q3 = T[3];
-    n = mk(q0.x, q0.y, q0.z);
-    float t = -(pt::dot(n, o) + q0.w) / pt::dot(n, d);
-    f3 v0 = mk(q1.x, q1.y, q1.z), v1 = mk(q2.x, q2.y, q2.z), v2 = mk(q3.x, q3.y, q3.z);
-    f3 p = o + d * t;
-    float e0 = pt::dot(n, pt::cross(v1 - v0, p - v0));
-    float e1 = pt::dot(n, pt::cross(v2 - v1, p - v1));
-    float e2 = pt::dot(n, pt::cross(v0 - v2, p - v2));
-    bool ok = !(t < 0.0f) && (t < tbest) && (e0 > 0.0f) && (e1 > 0.0f) && (e2 > 0.0f);
-    return ok ? t : -1.0f;
-}
-
-// Same test, but the plane distance is computed first and the edge tests run only if some
-// lane of the wave still needs them (a wave-uniform skip; per lane the verdict is the
-// same select as tri_hit_bf, so the bits are identical).
-template <bool LDS>
-__device__ __forceinline__ float tri_hit_lazy(const SceneView& S, int slot, float4 nd, f3 o, f3 d, float tbest,
-                                              f3& n) {
-    n = mk(nd.x, nd.y, nd.z);    // nd: quad 0 {n, d0}, loaded by the caller
-    float t = -(pt::dot(n, o) + nd.w) / pt::dot(n, d);
-    bool ok = !(t < 0.0f) && (t < tbest);
-    if (__any(ok)) {
-        const float4 q1 = tri_quad<LDS>(S, slot, 1), q2 = tri_quad<LDS>(S, slot, 2), q3 = tri_quad<LDS>(S, slot, 3);
-        f3 v0 = mk(q1.x, q1.y, q1.z), v1 = mk(q2.x, q2.y, q2.z), v2 = mk(q3.x, q3.y, q3.z);
-        f3 p = o + d * t;
-        float e0 = pt::dot(n, pt::cross(v1 - v0, p - v0));
-        float e1 = pt::dot(n, pt::cross(v2 - v1, p - v1));
-        float e2 = pt::dot(n, pt::cross(v0 - v2, p - v2));
-        ok = ok && (e0 > 0.0f) && (e1 > 0.0f) && (e2 > 0.0f);
-    }
-    return ok ? t : -1.0f;
-}
-
 // hit_triangle split in two for the leaf phase's edge-test compaction: the plane distance
 // (:285-297) and the three edge tests at that distance (:299-306), the same operations as
 // tri_hit_bf in the same order, so the same bits.
@@ -800,261 +509,8 @@ __device__ __forceinline__ void leaf_pair_tests(const SceneView& S, bool at, int
     h2 = okb ? tb : -1.0f;
 }
 
-// calculateRayCollision with "while-while" scheduling of the stackless walk: each lane
-// advances through the link chain until it reaches a leaf whose box it hits (or the walk
-// ends), and only then do the lanes that stopped at leaves run the two triangle tests
-// together.  Each lane still visits exactly the reference's node sequence and tests each
-// leaf before its next node, with the same t -- only the interleaving across lanes changes.
-template <bool COUNT>
-__device__ __forceinline__ bool collide_ww(const SceneView& S, int n_nodes, int n_spheres, int flags,
-                                           bool active, f3 o, f3 d, bool fast, f3 rd, f3& normal,
-                                           f3& hitp, int& mat, Cnt& c) {
-    float t = __builtin_huge_valf();
-    bool hit = false;
-    if (active && !(flags & PT_FLAG_NO_SPHERES)) {
-        for (int si = 0; si < n_spheres; si++) {
-            float4 s0 = S.spheres[2 * si];
-            f3 cc = mk(s0.x, s0.y, s0.z);
-            f3 oc = o - cc;
-            float a = pt::dot(d, d);
-            float half_b = pt::dot(oc, d);
-            float cq = pt::dot(oc, oc) - s0.w;
-            float disc = half_b * half_b - a * cq;
-            float ht = disc < 0.0f ? -1.0f : (-half_b - pt::fsqrt(disc)) / a;
-            if (COUNT) c.sph++;
-            if (ht > 0.0001f && ht < t) {
-                f3 pn = pt::normalize((o + d * ht) - cc);
-                if (pt::dot(pn, d) > 0.0f) pn = pn * -1.0f;
-                hit = true;
-                t = ht;
-                normal = pn;
-                hitp = o + d * ht;
-                mat = __float_as_int(S.spheres[2 * si + 1].x);
-            }
-        }
-    }
-    int bi = (active && !(flags & PT_FLAG_NO_TRIANGLES) && n_nodes > 0 && (COUNT || !ray_has_nan(o, d))) ? 0 : -1;
-    int steps = 0;
-    int leaf = 0;
-    bool pend = false;
-    for (;;) {
-        while (bi > -1 && !pend && steps < n_nodes) {
-            float4 lo = S.nodes[2 * bi], hi = S.nodes[2 * bi + 1];
-            int a = __float_as_int(hi.z), b = __float_as_int(hi.w);
-            bool hb = fast ? slab_fast(lo, hi, o, d, rd, t) : slab(lo, hi, o, d, t);
-            if (COUNT) { c.nodes++; diag_tick(c.tw, c.tl); }
-            steps++;
-            if (hb && a < 0) {
-                pend = true;
-                leaf = ~a;
-            }
-            bi = (hb && a >= 0) ? a : b;
-        }
-        if (!__any(pend)) break;
-        if (pend) {
-            if (COUNT) { c.tri += 2; diag_tick(c.lw, c.ll); }
-            const float4* T0 = S.tris + 8 * (leaf >> 2);
-            f3 n0, n1;
-            float h1, h2;
-            if (flags & PT_FLAG_MOLLER_TRUMBORE) {
-                n0 = mk(T0[0].x, T0[0].y, T0[0].z);
-                n1 = mk(T0[4].x, T0[4].y, T0[4].z);
-                h1 = tri_mt(T0[1], T0[2], T0[3], o, d);
-                h2 = tri_mt(T0[5], T0[6], T0[7], o, d);
-            } else {
-                h1 = tri_hit_bf(T0, o, d, t, n0);
-                h2 = tri_hit_bf(T0 + 4, o, d, t, n1);   // single-tri leaves hold a copy
-            }
-            bool c1 = h1 > 0.0001f && h1 < t && (h1 < h2 || h2 < 0.0001f);
-            bool c2 = !c1 && h2 > 0.0001f && h2 < t;
-            if (c1 || c2) {
-                f3 nn = c1 ? n0 : n1;
-                float th = c1 ? h1 : h2;
-                if (pt::dot(nn, d) > 0.0f) nn = nn * -1.0f;
-                hit = true;
-                t = th;
-                normal = nn;
-                hitp = o + d * th;
-                mat = __float_as_int(T0[c1 ? 2 : 6].w);
-            }
-            pend = false;
-        }
-    }
-    return hit;
-}
-
-template <bool COUNT, bool LDS, int MINW>
-__global__ __launch_bounds__(256, MINW) void k_render_wave(KParams p) {
-    resolve_frames(p);
-    extern __shared__ float4 lds[];
-    SceneView S;
-    if (LDS) {
-        int nn = 2 * p.sc.n_nodes, nt = 4 * p.n_slots, nm = 3 * p.n_mats, ns = 2 * p.sc.n_spheres;
-        for (int i = threadIdx.x; i < nn; i += blockDim.x) lds[i] = p.sc.nodes[i];
-        for (int i = threadIdx.x; i < nt; i += blockDim.x) lds[nn + i] = p.sc.tris[i];
-        for (int i = threadIdx.x; i < nm; i += blockDim.x) lds[nn + nt + i] = p.sc.mats[i];
-        for (int i = threadIdx.x; i < ns; i += blockDim.x) lds[nn + nt + nm + i] = p.sc.spheres[i];
-        __syncthreads();
-        S.nodes = lds;
-        S.tris = lds + nn;
-        S.mats = lds + nn + nt;
-        S.spheres = lds + nn + nt + nm;
-    } else {
-        S.nodes = p.sc.nodes;
-        S.tris = p.sc.tris;
-        S.mats = p.sc.mats;
-        S.spheres = p.sc.spheres;
-    }
-    const int lane = threadIdx.x & 63;
-    const f3 cpos = mk(p.cam[0], p.cam[1], p.cam[2]), cfwd = mk(p.cam[3], p.cam[4], p.cam[5]);
-    const f3 cright = mk(p.cam[6], p.cam[7], p.cam[8]), cup = mk(p.cam[9], p.cam[10], p.cam[11]);
-    const int tiles_x = (p.W + 7) >> 3;
-    const unsigned total_ids = (unsigned)tiles_x * (unsigned)((p.rows_local + 7) >> 3) * 64u;
-    const bool origin0_ok = p.scene_fast && in_guard(cpos.x, 0x1p-40f, 0x1p60f) &&
-                            in_guard(cpos.y, 0x1p-40f, 0x1p60f) && in_guard(cpos.z, 0x1p-40f, 0x1p60f);
-
-    Cnt c = {0, 0, 0, 0, 0};
-    bool done = false, need_path = true;
-    int lx = -1, y = 0;
-    size_t aidx = 0;
-    int k = 0, r = 0, bounce = 0;
-    float4 acc = make_float4(0, 0, 0, 0);
-    f3 psum = mk(0, 0, 0), o = mk(0, 0, 0), d = mk(0, 0, 1), inc = mk(0, 0, 0), col = mk(1, 1, 1);
-    uint32_t state = 0;
-
-    for (;;) {
-        // (1) release a pixel whose frames are all done
-        if (!done && need_path && lx >= 0 && k >= p.n_frames) {
-            p.accum[aidx] = acc;
-            lx = -1;
-        }
-        // (2) wave-aggregated pull from the pixel queue
-        bool want = !done && lx < 0;
-        unsigned long long m = __ballot(want);
-        if (m) {
-            int leader = __ffsll((long long)m) - 1;
-            unsigned base = 0;
-            if (lane == leader) base = atomicAdd(p.work_counter, (unsigned)__popcll(m));
-            base = __shfl(base, leader, 64);
-            if (want) {
-                unsigned id = base + (unsigned)__popcll(m & ((1ull << lane) - 1ull));
-                if (id >= total_ids) {
-                    done = true;
-                } else {
-                    unsigned tile = id >> 6, w = id & 63u;
-                    int cx = (int)(tile % (unsigned)tiles_x) * 8 + (int)(w & 7u);
-                    int crow = (int)(tile / (unsigned)tiles_x) * 8 + (int)(w >> 3);
-                    int cy = p.row0 + crow * p.row_stride;
-                    if (cx < p.W && crow < p.rows_local && cx < p.x_limit && cy < p.y_limit) {
-                        lx = cx;
-                        y = cy;
-                        aidx = (size_t)crow * p.W + cx;
-                        k = 0;
-                        r = 0;
-                        psum = mk(0, 0, 0);
-                        acc = p.acc_first ? p.accum[aidx] : make_float4(0, 0, 0, 0);
-                        need_path = true;
-                    }
-                }
-            }
-        }
-        // (3) camera ray for the next (frame, ray) of this lane's pixel (:514-542)
-        if (!done && lx >= 0 && need_path) {
-            if (r == 0) state = pt::seed(lx, y, p.frame_first + k);
-            float ax = 0.0f, ay = 0.0f;
-            if (!(p.flags & PT_FLAG_NO_AA)) {
-                ax = pt::random01(state);
-                ay = pt::random01(state);
-            }
-            float u = ((float)lx + ax) / (float)p.W - 0.5f;
-            float v = ((float)y + ay) / (float)p.H - 0.5f;
-            d = pt::normalize((cfwd + cright * u) + cup * v);
-            o = cpos;
-            inc = mk(0, 0, 0);
-            col = mk(1, 1, 1);
-            bounce = 0;
-            need_path = false;
-        }
-        bool busy = !done && lx >= 0 && !need_path;
-        if (__ballot(!done) == 0ull) break;
-        if (!__any(busy)) continue;
-
-        // (4) one segment: calculateRayCollision + the body of Trace's loop (:447-498)
-        bool fast = (bounce == 0 ? origin0_ok
-                                 : (p.scene_fast && in_guard(o.x, 0x1p-40f, 0x1p60f) &&
-                                    in_guard(o.y, 0x1p-40f, 0x1p60f) && in_guard(o.z, 0x1p-40f, 0x1p60f))) &&
-                    in_guard(d.x, 0x1p-20f, 2.0f) && d.x != 0.0f && in_guard(d.y, 0x1p-20f, 2.0f) && d.y != 0.0f &&
-                    in_guard(d.z, 0x1p-20f, 2.0f) && d.z != 0.0f;
-        f3 rd = mk(0, 0, 0);
-        if (fast) rd = mk(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
-        f3 normal = mk(0, 0, 0), hitp = mk(0, 0, 0);
-        int mat = 0;
-        bool hit = collide_ww<COUNT>(S, p.sc.n_nodes, p.sc.n_spheres, p.flags, busy, o, d, fast, rd, normal,
-                                     hitp, mat, c);
-        if (!busy) continue;
-        if (COUNT) { c.seg++; if (hit) c.hits++; diag_tick(c.sw, c.sl); }
-        bool finished = false;
-        f3 rgb = inc;
-        if (hit && pt::length(col) > 0.01f) {
-            if (p.mode == 2) {
-                rgb = (normal + mk(1, 1, 1)) * 0.5f;
-                finished = true;
-            } else if (p.mode == 4) {
-                float s = pt::length(hitp - o);
-                float dist = 1.0f - pt::fsqrt(s + 1.0f) / (s + 1.0f);
-                float q = dist * dist;
-                rgb = mk(q, q, q);
-                finished = true;
-            } else {
-                o = hitp;
-                f3 diffuse = pt::normalize(normal + pt::random_unit_vector(state));
-                float kk = 2.0f * pt::dot(normal, d);
-                f3 specular = pt::normalize(d - normal * kk);
-                float4 m0 = S.mats[3 * mat], m1 = S.mats[3 * mat + 1], m2 = S.mats[3 * mat + 2];
-                if (p.mode == 3) {
-                    rgb = mk(m0.x, m0.y, m0.z);
-                    finished = true;
-                } else {
-                    float is_spec = (m1.w > pt::random01(state)) ? 1.0f : 0.0f;
-                    d = pt::mix(diffuse, specular, m0.w * is_spec);
-                    inc = inc + mk(m1.x, m1.y, m1.z) * col;
-                    col = col * pt::mix(mk(m0.x, m0.y, m0.z), mk(m2.x, m2.y, m2.z), is_spec);
-                    bounce++;
-                    if (bounce > p.max_bounce) {
-                        rgb = inc;
-                        finished = true;
-                    }
-                }
-            }
-        } else {
-            f3 env = mk(0, 0, 0);
-            if (!(p.flags & PT_FLAG_NO_SKY)) {
-                f3 dir = pt::normalize(d);
-                float tt = 0.5f * (dir.z + 1.0f);
-                float omt = 1.0f - tt;
-                env = mk(omt * 1.0f + tt * 0.5f, omt * 1.0f + tt * 0.7f, omt * 1.0f + tt * 1.0f);
-            }
-            rgb = inc + env * col;
-            finished = true;
-        }
-        if (finished) {
-            psum = psum + rgb;
-            r++;
-            if (r >= p.rpp) {
-                int f = p.frame_first + k;
-                acc = accumulate(acc, psum / (float)p.rpp, f, k > 0 || p.acc_first == 1);
-                psum = mk(0, 0, 0);
-                r = 0;
-                k++;
-            }
-            need_path = true;
-        }
-    }
-    flush_counters<COUNT>(p, c);
-}
-
 // =====================================================================================
-// Variant 6: persistent state-machine kernel.  Every lane carries one path through three
+// The state machine (variants 0 and 3).  Every lane carries one path through three
 // states -- TRAV (walking the link chain), LEAF (stopped at a leaf whose box it hit), SHADE
 // (segment finished: shade / regenerate / set up the next segment) -- and each wave
 // iteration runs ONE phase for the lanes in that state, picked by ballot counts:
@@ -1066,9 +522,6 @@ __global__ __launch_bounds__(256, MINW) void k_render_wave(KParams p) {
 // =====================================================================================
 enum : int { ST_DONE = 0, ST_TRAV = 1, ST_LEAF = 2, ST_SHADE = 3 };
 constexpr unsigned kPullBatch = 32;
-#ifndef PT_LEAF_COMPACT
-#define PT_LEAF_COMPACT 1   // leaf phase: edge tests compacted over the wave (leaf_pair_tests)
-#endif
 #ifndef PT_WALK_UNROLL
 #define PT_WALK_UNROLL 4
 #endif
@@ -1558,15 +1011,7 @@ __global__ __launch_bounds__(NT, MINW) void k_render_sm(KParams p) {
                                 tri_quad<LDS>(S, s0 + 1, 3), o, d);
                 }
             } else {
-#if PT_LEAF_COMPACT
                 leaf_pair_tests<LDS>(S, at, s0, nd0, cop, o, d, t, p.compact_max, h1, h2);
-#else
-                if (at) {
-                    f3 n0, n1;
-                    h1 = tri_hit_lazy<LDS>(S, s0, nd0, o, d, t, n0);
-                    h2 = tri_hit_lazy<LDS>(S, s0 + 1, tri_quad<LDS>(S, s0 + 1, 0), o, d, t, n1);
-                }
-#endif
             }
             bool c1 = false, c2 = false;
             if (at) {
@@ -1689,593 +1134,6 @@ __global__ __launch_bounds__(256) void k_accum_frames(KParams p) {
     p.accum[idx] = acc;
 }
 
-// =====================================================================================
-// Variant 4: wavefront kernel with workgroup queues (LDS-staged scenes).
-//
-// The state-machine kernel ties a path to one lane for its whole life, so a wave walks,
-// leaf-tests or shades with only the lanes in that state (measured on C2: 44% / 70% / 73%
-// of the lanes).  Here the paths live in LDS records, one per path slot, and waves are
-// workers: a wave keeps up to 64 rays walking in registers and refills lanes from a walk
-// queue as rays stop; rays that stop at a hit leaf go to a leaf queue, rays whose walk ended
-// to a shade queue, and any wave takes batches of 64 from those queues (leaf tests / shading
-// + path regeneration), pushing the rays back to the walk queue.  Every path still runs the
-// reference's operations in the reference's order (node, its leaf's tests before the next
-// node, the same t; frames in order through the frame-colour buffer), so the image is the
-// same bits; only which lane executes which step changes.
-//
-// One workgroup of 16 waves per CU shares one scene copy and P path slots:
-//   ray record  (3 float4 planes): {o, t}, {d, hprim}, {rd, w}   (rd = 0: outside the guard)
-//   path record (3 float4 planes): {col, rng}, {inc, x | y << 16}, {pixel, k | kend << 16,
-//                                   bounce | flags << 8 | segments << 16, tile}
-//   queues: rings of (slot + 1) in u16, 0 = not yet written, with per-queue {tail, head,
-//   avail} counters; `avail` counts published entries, a pop reserves from it first.
-// =====================================================================================
-constexpr int kWfQW = 0, kWfQL = 1, kWfQS = 2; // walk, leaf, shade queues
-constexpr unsigned kWfChunk = 256;             // work ids a workgroup takes from the device queue at once
-constexpr int kWfLive = 9;                     // counter: path slots not yet retired
-constexpr unsigned kWfFresh = 1u, kWfNeedRay = 2u, kWfHasPx = 4u;
-
-#ifdef PT_WF_DIAG
-// experiment builds only (-DPT_WF_DIAG): per-wave counters of the wavefront kernel, read back
-// by pt_debug_wf_diag: [0] walk wave-steps, [1] walk lane-steps, [2] leaf batches, [3] leaf
-// lanes, [4] shade batches, [5] shade lanes, [6] idle sleeps, [7..10] clocks walk / leaf /
-// shade / idle, [11] refilled lanes, [12] pops that waited for an entry
-__device__ unsigned long long g_wf_diag[16];
-struct WfDiag {
-    unsigned long long v[16] = {};
-    __device__ void add(int i, unsigned long long x) { v[i] += x; }
-    __device__ void flush() {
-        if (lane_id() == 0)
-            for (int i = 0; i < 16; i++) atomicAdd(&g_wf_diag[i], v[i]);
-    }
-};
-#else
-struct WfDiag {
-    __device__ void add(int, unsigned long long) {}
-    __device__ void flush() {}
-};
-#endif
-#define WF_DIAG(i, v) dg.add(i, (unsigned long long)(v))
-typedef __attribute__((address_space(3))) unsigned lds_u32;
-typedef __attribute__((address_space(3))) unsigned short lds_u16;
-typedef __attribute__((address_space(3))) v4f lds_v4;
-
-struct WfLds {
-    int r0, r1, r2, q0, q1, q2;   // float4 plane bases
-    unsigned ring;                // byte offset of the 3 rings (rmask + 1 entries each)
-    unsigned rmask;
-    unsigned ctr;                 // byte offset of the counters
-};
-__device__ __forceinline__ v4f wf_ld(int plane, int s) { return *(lds_v4*)(size_t)(unsigned)((plane + s) << 4); }
-__device__ __forceinline__ void wf_st(int plane, int s, v4f v) { *(lds_v4*)(size_t)(unsigned)((plane + s) << 4) = v; }
-__device__ __forceinline__ void wf_stw(int plane, int s, float v) {   // .w only
-    *(__attribute__((address_space(3))) float*)(size_t)(unsigned)(((plane + s) << 4) + 12) = v;
-}
-__device__ __forceinline__ lds_u32* wf_ctr(const WfLds& L, int i) { return (lds_u32*)(size_t)(L.ctr + 4u * i); }
-__device__ __forceinline__ unsigned wf_peek(const WfLds& L, int i) {    // wave-uniform read
-    return (unsigned)__builtin_amdgcn_readfirstlane((int)*(volatile lds_u32*)wf_ctr(L, i));
-}
-
-// Pushes the slot of every lane with m set onto queue q (records written before the call).
-__device__ __forceinline__ void wf_push(const WfLds& L, int q, bool m, int slot) {
-    const unsigned long long b = __ballot(m);
-    if (!b) return;
-    const int n = __popcll(b), leader = __ffsll((long long)b) - 1;
-    const int lane = lane_id();
-    unsigned base = 0;
-    if (lane == leader) base = __hip_atomic_fetch_add(wf_ctr(L, 3 * q), (unsigned)n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-    base = (unsigned)__builtin_amdgcn_readlane((int)base, leader);
-    if (m) {
-        const unsigned pos = (base + (unsigned)rank_in(b)) & L.rmask;
-        *(volatile lds_u16*)(size_t)(L.ring + 2u * ((unsigned)q * (L.rmask + 1u) + pos)) = (unsigned short)(slot + 1);
-    }
-    // the records and ring entries must be in LDS before the entries are published (the LDS
-    // executes one wave's operations in order; the barrier keeps the compiler from sinking the
-    // stores below the publishing atomic)
-#ifdef PT_WF_NOWAIT
-    asm volatile("" ::: "memory");
-#else
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-#endif
-    if (lane == leader) __hip_atomic_fetch_add(wf_ctr(L, 3 * q + 2), (unsigned)n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-}
-
-// Pops up to popcount(want) published entries of queue q for the lanes in `want` (in lane
-// order); a lane that gets none returns -1.
-// `strict`: all popcount(want) entries or none.
-__device__ __forceinline__ int wf_pop(const WfLds& L, int q, unsigned long long want, unsigned* err, WfDiag& dg,
-                                     bool strict = false) {
-    const int n = __popcll(want);
-    if (!n) return -1;
-    const int leader = __ffsll((long long)want) - 1;
-    const int lane = lane_id();
-    int got = 0;
-    unsigned head = 0;
-    if (lane == leader) {
-        const int a = (int)__hip_atomic_fetch_add(wf_ctr(L, 3 * q + 2), (unsigned)-n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-        got = a >= n ? n : (a > 0 && !strict ? a : 0);
-        if (got < n) __hip_atomic_fetch_add(wf_ctr(L, 3 * q + 2), (unsigned)(n - got), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-        if (got) head = __hip_atomic_fetch_add(wf_ctr(L, 3 * q + 1), (unsigned)got, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-    }
-    got = __builtin_amdgcn_readlane(got, leader);
-    head = (unsigned)__builtin_amdgcn_readlane((int)head, leader);
-    const int r = rank_in(want);
-    int slot = -1;
-    if (((want >> lane) & 1ull) && r < got) {
-        volatile lds_u16* e = (volatile lds_u16*)(size_t)(L.ring + 2u * ((unsigned)q * (L.rmask + 1u) + ((head + (unsigned)r) & L.rmask)));
-        unsigned v = *e;
-        if (v == 0u) {               // reserved by a producer that has not written it yet
-            WF_DIAG(12, 1);
-            const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
-            while (v == 0u) {
-                __builtin_amdgcn_s_sleep(1);
-                v = *e;
-                // watchdog (100 MHz clock): a producer never takes 1 s to write its entry
-                if (v == 0u && __builtin_amdgcn_s_memrealtime() - t0 > 100000000ull) {
-                    atomicAdd(err, 1u);
-                    return -1;
-                }
-            }
-        }
-        *e = 0;
-        slot = (int)v - 1;
-    }
-    return slot;
-}
-
-// The walk of the wavefront kernel: the lanes with w >= 0 take node steps (bvh_intersect +
-// the link choice, WalkLinks) until at most `refill` of them still walk.
-// LDS scenes walk the octant images (WalkLinks); global-memory scenes the reference links
-// (node indices; a leaf's hit link ~code becomes -2 - code), top nodes from LDS.
-template <bool ALL_FAST, bool LDS, bool PADN>
-__device__ __forceinline__ void wf_walk(const SceneView& S, f3 o, f3 d, f3 rd, bool fast, float t, int refill,
-                                        int& w, WfDiag& dg) {
-    for (;;) {
-#pragma unroll
-        for (int u = 0; u < kWalkUnroll; u++) {
-#ifdef PT_WF_DIAG
-            { const unsigned long long mm = __ballot(w >= 0); if (mm) { WF_DIAG(0, 1); WF_DIAG(1, __popcll(mm)); } }
-#endif
-            if (w >= 0) {
-                float4 lo, hi;
-                node_at<LDS, PADN>(S, w, lo, hi);
-                const int a = __float_as_int(hi.z), b = __float_as_int(hi.w);
-                const bool hb = (ALL_FAST || fast) ? (LDS ? slab_oct(lo, hi, o, d, rd, t) : slab_fast(lo, hi, o, d, rd, t))
-                                                   : slab(lo, hi, o, d, t);
-                w = hb ? (LDS || a >= 0 ? a : a - 1) : b;
-            }
-        }
-        if (__popcll(__ballot(w >= 0)) <= refill) break;
-    }
-}
-
-// Leaf batch: up to 64 rays from the leaf queue, both triangle tests + the 2-way choice
-// (:406-429), then back to the walk queue at the leaf's continuation (or to the shade queue).
-template <bool LDS>
-__device__ __forceinline__ bool wf_leaf_batch(const KParams& p, const SceneView& S, const WfLds& L, WfDiag& dg,
-                                              bool strict) {
-    const int s = wf_pop(L, kWfQL, ~0ull, p.wf_err, dg, strict);
-    const bool at = s >= 0;
-    if (!__any(at)) return false;
-    WF_DIAG(2, 1);
-    WF_DIAG(3, __popcll(__ballot(at)));
-    const int si = at ? s : 0;
-    const v4f a0 = wf_ld(L.r0, si), a1 = wf_ld(L.r1, si), a2 = wf_ld(L.r2, si);
-    const f3 o = mk(a0.x, a0.y, a0.z), d = mk(a1.x, a1.y, a1.z);
-    float t = a0.w;
-    int hprim = __float_as_int(a1.w);
-    const bool fast = a2.x != 0.0f;
-    const int code = at ? -2 - __float_as_int(a2.w) : 0;    // k << 2 | coplanar << 1 | single
-    const int s0 = (code >> 1) & ~1;
-    const float4 nd0 = tri_quad<LDS>(S, s0, 0);
-    // the leaf's next-right: LDS image-0 byte offset (quad 1 .w, + the ray's octant image) or
-    // global node index (quad 3 .w)
-    int cont = __float_as_int(tri_quad<LDS>(S, s0, LDS ? 1 : 3).w);
-    if (LDS && (fast & (cont >= 0))) cont += oct_base(d, S.np << 5);
-    float h1 = -1.0f, h2 = -1.0f;
-    if (p.flags & PT_FLAG_MOLLER_TRUMBORE) {
-        if (at) {
-            h1 = tri_mt(tri_quad<LDS>(S, s0, 1), tri_quad<LDS>(S, s0, 2), tri_quad<LDS>(S, s0, 3), o, d);
-            h2 = tri_mt(tri_quad<LDS>(S, s0 + 1, 1), tri_quad<LDS>(S, s0 + 1, 2), tri_quad<LDS>(S, s0 + 1, 3), o, d);
-        }
-    } else {
-        leaf_pair_tests<LDS>(S, at, s0, nd0, (code & 2) != 0, o, d, t, p.compact_max, h1, h2);
-    }
-    if (at) {
-        const bool c1 = (h1 > 0.0001f) & (h1 < t) & ((h1 < h2) | (h2 < 0.0001f));
-        const bool c2 = !c1 & (h2 > 0.0001f) & (h2 < t);
-        if (c1 | c2) {
-            t = c1 ? h1 : h2;
-            hprim = s0 + (c1 ? 0 : 1);
-            wf_stw(L.r0, s, t);
-            wf_stw(L.r1, s, __int_as_float(hprim));
-        }
-        wf_stw(L.r2, s, __int_as_float(cont));
-    }
-    wf_push(L, kWfQW, at & (cont >= 0), s);
-    wf_push(L, kWfQS, at & (cont < 0), s);
-    return true;
-}
-
-// Shade batch: up to 64 paths from the shade queue.  Finishes their segments (the body of
-// Trace's loop, :447-498), stores finished frames' colours, regenerates finished paths
-// (next frame of the work item, or a new item from the device queue), sets up the next
-// segment (guard, spheres :372-385, walk start) and queues it.  The operations are those of
-// k_render_sm's SHADE phase for one path.
-template <bool LDS>
-__device__ __forceinline__ bool wf_shade_batch(const KParams& p, const SceneView& S, const WfLds& L,
-                                               unsigned total_ids, unsigned n_groups, int root_skip, WfDiag& dg,
-                                               bool strict) {
-    const int s = wf_pop(L, kWfQS, ~0ull, p.wf_err, dg, strict);
-    bool act = s >= 0;
-    if (!__any(act)) return false;
-    WF_DIAG(4, 1);
-    WF_DIAG(5, __popcll(__ballot(act)));
-    const int si = act ? s : 0;
-    const v4f a0 = wf_ld(L.r0, si), a1 = wf_ld(L.r1, si);
-    const v4f b0 = wf_ld(L.q0, si), b1 = wf_ld(L.q1, si), b2 = wf_ld(L.q2, si);
-    f3 o = mk(a0.x, a0.y, a0.z), d = mk(a1.x, a1.y, a1.z);
-    float t = a0.w;
-    int hprim = __float_as_int(a1.w);
-    f3 col = mk(b0.x, b0.y, b0.z), inc = mk(b1.x, b1.y, b1.z);
-    uint32_t state = __float_as_uint(b0.w);
-    const unsigned lxy = __float_as_uint(b1.w);
-    int lx = (int)(lxy & 0xffffu), y = (int)(lxy >> 16);
-    int aidx = (int)__float_as_uint(b2.x);
-    int k = (int)(__float_as_uint(b2.y) & 0xffffu), kend = (int)(__float_as_uint(b2.y) >> 16);
-    const unsigned bfl = __float_as_uint(b2.z);
-    int bounce = (int)(bfl & 0xffu);
-    unsigned flags = (bfl >> 8) & 0xffu, pcost = bfl >> 16;
-    unsigned tile_id = __float_as_uint(b2.w);
-    bool need_ray = (flags & kWfNeedRay) != 0u, has_px = (flags & kWfHasPx) != 0u;
-
-    if (act && !(flags & kWfFresh)) {
-        const bool hit = hprim != -1;
-        pcost++;
-        bool finished = false;
-        f3 rgb = inc;
-        if (hit && pt::length_gt_001(col)) {
-            const f3 hitp = o + d * t;
-            f3 normal;
-            int mat;
-            if (hprim >= 0) {
-                const float4 nq = tri_quad<LDS>(S, hprim, 0);
-                normal = mk(nq.x, nq.y, nq.z);
-                mat = __float_as_int(tri_quad<LDS>(S, hprim, 2).w);
-            } else {
-                const int sph = -2 - hprim;
-                const float4 c0 = S.spheres[2 * sph];
-                normal = pt::normalize(hitp - mk(c0.x, c0.y, c0.z));
-                mat = __float_as_int(S.spheres[2 * sph + 1].x);
-            }
-            if (pt::dot(normal, d) > 0.0f) normal = normal * -1.0f;
-            if (p.mode == 2) {
-                rgb = (normal + mk(1, 1, 1)) * 0.5f;
-                finished = true;
-            } else if (p.mode == 4) {
-                const float sd = pt::length(hitp - o);
-                const float dist = 1.0f - pt::fsqrt(sd + 1.0f) / (sd + 1.0f);
-                const float q = dist * dist;
-                rgb = mk(q, q, q);
-                finished = true;
-            } else {
-                o = hitp;
-                const f3 diffuse = pt::normalize(normal + pt::random_unit_vector(state));
-                const float kk = 2.0f * pt::dot(normal, d);
-                const f3 specular = pt::normalize(d - normal * kk);
-                const float4 m0 = S.mats[3 * mat], m1 = S.mats[3 * mat + 1], m2 = S.mats[3 * mat + 2];
-                if (p.mode == 3) {
-                    rgb = mk(m0.x, m0.y, m0.z);
-                    finished = true;
-                } else {
-                    const float is_spec = (m1.w > pt::random01(state)) ? 1.0f : 0.0f;
-                    d = pt::mix(diffuse, specular, m0.w * is_spec);
-                    inc = inc + mk(m1.x, m1.y, m1.z) * col;
-                    col = col * pt::mix(mk(m0.x, m0.y, m0.z), mk(m2.x, m2.y, m2.z), is_spec);
-                    bounce++;
-                    if (bounce > p.max_bounce) {
-                        rgb = inc;
-                        finished = true;
-                    }
-                }
-            }
-        } else {
-            f3 env = mk(0, 0, 0);
-            if (!(p.flags & PT_FLAG_NO_SKY)) {
-                const f3 dir = pt::normalize(d);
-                const float tt = 0.5f * (dir.z + 1.0f);
-                const float omt = 1.0f - tt;
-                env = mk(omt * 1.0f + tt * 0.5f, omt * 1.0f + tt * 0.7f, omt * 1.0f + tt * 1.0f);
-            }
-            rgb = inc + env * col;
-            finished = true;
-        }
-        need_ray = finished;
-        if (finished) {   // raysPerPixel == 1: pixel = (0 + rgb) / 1 (:541-546)
-            const f3 px = (mk(0, 0, 0) + rgb) / 1.0f;
-            nt_store3(p.rgb + 3 * ((size_t)k * (size_t)(p.rows_local * p.W) + (size_t)aidx), px);
-            k++;
-        }
-    }
-    flags = kWfFresh;          // the finished segment (if any) is consumed
-    if (act & need_ray & has_px & (k >= kend)) {      // work item done: release the pixel
-        if (p.tile_cost && tile_id != ~0u) atomicAdd(&p.tile_cost[tile_id], pcost);
-        has_px = false;
-    }
-    // wave-aggregated pull from the device work queue: exactly the ids this batch hands out
-    // (any wave may shade any slot, so a wave must not keep reserved ids for later)
-    const bool want = act & !has_px;
-    const unsigned long long m = __ballot(want);
-    if (m) {
-        const unsigned need = (unsigned)__popcll(m);
-        const unsigned rank = (unsigned)rank_in(m);
-        const int leader = __ffsll((long long)m) - 1;
-        // the workgroup's id pool (counters 10 = next id, 11 = ids left, 12 = lock): a device
-        // atomic only once per kWfChunk ids (its return is a long stall); the ids of one pull
-        // may come from the old pool and a fresh chunk
-        unsigned base0 = 0, take0 = 0, base1 = 0;
-        if (want && rank == 0u) {
-            unsigned expected = 0u;
-            while (!__hip_atomic_compare_exchange_strong(wf_ctr(L, 12), &expected, 1u, __ATOMIC_RELAXED,
-                                                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) {
-                expected = 0u;
-                __builtin_amdgcn_s_sleep(1);
-            }
-            unsigned nx = *(volatile lds_u32*)wf_ctr(L, 10), left = *(volatile lds_u32*)wf_ctr(L, 11);
-            take0 = min(need, left);
-            base0 = nx;
-            nx += take0;
-            left -= take0;
-            if (take0 < need) {
-                base1 = atomicAdd(p.work_counter, kWfChunk);
-                nx = base1 + (need - take0);
-                left = kWfChunk - (need - take0);
-            }
-            *(volatile lds_u32*)wf_ctr(L, 10) = nx;
-            *(volatile lds_u32*)wf_ctr(L, 11) = left;
-            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-            *(volatile lds_u32*)wf_ctr(L, 12) = 0u;
-        }
-        base0 = (unsigned)__builtin_amdgcn_readlane((int)base0, leader);
-        take0 = (unsigned)__builtin_amdgcn_readlane((int)take0, leader);
-        base1 = (unsigned)__builtin_amdgcn_readlane((int)base1, leader);
-        const unsigned id = rank < take0 ? base0 + rank : base1 + (rank - take0);
-        if (want) {
-            if (id >= total_ids) {
-                act = false;       // queue exhausted: the slot retires
-                __hip_atomic_fetch_add(wf_ctr(L, kWfLive), (unsigned)-1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-            } else {
-                const unsigned item = id >> 6, wl = id & 63u;
-                unsigned tile = p.grp_magic ? __umulhi(item, p.grp_magic) : item / n_groups;
-                const int g = (int)(item - tile * n_groups);
-                const int tiles_x = (p.W + 7) >> 3;
-                int tx, ty;
-                if (p.tile_perm) {
-                    const unsigned pk = p.tile_perm[tile];
-                    tx = (int)(pk & 0xffffu);
-                    ty = (int)(pk >> 16);
-                } else {
-                    tx = (int)(tile % (unsigned)tiles_x);
-                    ty = (int)(tile / (unsigned)tiles_x);
-                }
-                tile = (unsigned)(ty * tiles_x + tx);
-                const int cx = tx * 8 + (int)(wl & 7u), crow = ty * 8 + (int)(wl >> 3);
-                const int cy = p.row0 + crow * p.row_stride;
-                if ((cx < p.W) & (crow < p.rows_local) & (cx < p.x_limit) & (cy < p.y_limit)) {
-                    lx = cx;
-                    y = cy;
-                    aidx = crow * p.W + cx;
-                    tile_id = ((wl & 0x1bu) == 0u) ? tile : ~0u;
-                    pcost = 0;
-                    k = g * p.group;
-                    kend = min(k + p.group, p.n_frames);
-                    need_ray = true;
-                    has_px = true;
-                }
-                // an id outside the image: the slot asks again in a later batch
-            }
-        }
-    }
-    bool walk = false;
-    int w = -1;
-    f3 rd = mk(0, 0, 0);
-    if (act & has_px) {
-        if (need_ray) {           // camera ray (:514-542)
-            state = pt::seed(lx, y, p.frame_first + k);
-            float ax = 0.0f, ay = 0.0f;
-            if (!(p.flags & PT_FLAG_NO_AA)) {
-                ax = pt::random01(state);
-                ay = pt::random01(state);
-            }
-            const float u = pt::div_mk((float)lx + ax, p.fW, p.rW) - 0.5f;
-            const float v = pt::div_mk((float)y + ay, p.fH, p.rH) - 0.5f;
-            const f3 cfwd = mk(p.cam[3], p.cam[4], p.cam[5]), cright = mk(p.cam[6], p.cam[7], p.cam[8]);
-            const f3 cup = mk(p.cam[9], p.cam[10], p.cam[11]);
-            d = pt::normalize((cfwd + cright * u) + cup * v);
-            o = mk(p.cam[0], p.cam[1], p.cam[2]);
-            inc = mk(0, 0, 0);
-            col = mk(1, 1, 1);
-            bounce = 0;
-            need_ray = false;
-        }
-        // segment set-up: exact-reciprocal guard, spheres (:372-385), walk start
-        const bool fast = (p.scene_fast != 0) & in_guard(o.x, 0x1p-40f, 0x1p60f) & in_guard(o.y, 0x1p-40f, 0x1p60f) &
-                          in_guard(o.z, 0x1p-40f, 0x1p60f) & in_range_abs(d.x, 0x1p-20f, 2.0f) &
-                          in_range_abs(d.y, 0x1p-20f, 2.0f) & in_range_abs(d.z, 0x1p-20f, 2.0f);
-        if (fast) rd = mk(pt::rcp_fast(d.x), pt::rcp_fast(d.y), pt::rcp_fast(d.z));
-        t = __builtin_huge_valf();
-        hprim = -1;
-        if (!(p.flags & PT_FLAG_NO_SPHERES)) {
-            for (int sp = 0; sp < p.sc.n_spheres; sp++) {
-                const float4 c0 = S.spheres[2 * sp];
-                const f3 oc = o - mk(c0.x, c0.y, c0.z);
-                const float a = pt::dot(d, d);
-                const float half_b = pt::dot(oc, d);
-                const float cq = pt::dot(oc, oc) - c0.w;
-                const float disc = half_b * half_b - a * cq;
-                const float ht = disc < 0.0f ? -1.0f : pt::div_g(-half_b - pt::sqrt_g(disc), a);
-                if ((ht > 0.0001f) & (ht < t)) {
-                    t = ht;
-                    hprim = -2 - sp;
-                }
-            }
-        }
-        walk = !(p.flags & PT_FLAG_NO_TRIANGLES) & (p.sc.n_nodes > 0) & !ray_has_nan(o, d);
-        const bool inside = (root_skip >= 0) & fast & (o.x >= p.root_box[0]) & (o.x <= p.root_box[1]) &
-                            (o.y >= p.root_box[2]) & (o.y <= p.root_box[3]) & (o.z >= p.root_box[4]) &
-                            (o.z <= p.root_box[5]);
-        const int img = (LDS && fast) ? oct_base(d, S.np << 5) : 0;
-        w = walk ? (inside ? root_skip : 0) + img : -1;
-        flags = 0u;                // a segment is set up: the next batch finishes it
-    }
-    if (act) {
-        flags |= (need_ray ? kWfNeedRay : 0u) | (has_px ? kWfHasPx : 0u);
-        wf_st(L.r0, s, v4f{o.x, o.y, o.z, t});
-        wf_st(L.r1, s, v4f{d.x, d.y, d.z, __int_as_float(hprim)});
-        wf_st(L.r2, s, v4f{rd.x, rd.y, rd.z, __int_as_float(w)});
-        wf_st(L.q0, s, v4f{col.x, col.y, col.z, __uint_as_float(state)});
-        wf_st(L.q1, s, v4f{inc.x, inc.y, inc.z, __uint_as_float((unsigned)lx | ((unsigned)y << 16))});
-        wf_st(L.q2, s, v4f{__uint_as_float((unsigned)aidx), __uint_as_float((unsigned)k | ((unsigned)kend << 16)),
-                           __uint_as_float((unsigned)bounce | (flags << 8) | (pcost << 16)), __uint_as_float(tile_id)});
-    }
-    // walking segments to the walk queue; a slot still without a pixel (an id outside the
-    // image) or a segment without a walk goes back to the shade queue
-    wf_push(L, kWfQW, act & walk, s);
-    wf_push(L, kWfQS, act & !walk, s);
-    return true;
-}
-
-// NT threads per workgroup; MINW = resident waves per SIMD (the register budget)
-// LDS: the scene staged as in k_render_sm; !LDS (global-memory scene): the top p.n_top
-// nodes, the materials and the spheres in LDS, nodes below and the triangles in global
-// memory.  The path records follow in either case.
-template <bool LDS, bool PADN, int NT, int MINW>
-__global__ __launch_bounds__(NT, MINW) void k_render_wf(KParams p) {
-    resolve_frames(p);
-    extern __shared__ float4 lds[];
-    if ((unsigned)(size_t)(__attribute__((address_space(3))) const char*)g_lds != 0u) __builtin_trap();
-    const int N = LDS ? (PADN ? kPadNodes : p.walk_np) : p.n_top, T = p.n_slots;
-    const int nn = LDS ? 16 * N : 2 * N, nt = LDS ? 4 * T : 0;
-    const int nm = 3 * p.n_mats, ns = 2 * p.sc.n_spheres;
-    const int tid = threadIdx.x;
-    if (LDS) {
-        for (int i = tid; i < nn; i += NT) lds[i] = p.sc.walk_lds[i];
-        for (int i = tid; i < nt; i += NT) lds[nn + (i & 3) * T + (i >> 2)] = p.sc.tris[i];
-    } else {   // top nodes in planes: lo at [i], hi at [N + i]
-        for (int i = tid; i < nn; i += NT) lds[(i & 1) * N + (i >> 1)] = p.sc.nodes[i];
-    }
-    for (int i = tid; i < nm; i += NT) lds[nn + nt + i] = p.sc.mats[i];
-    for (int i = tid; i < ns; i += NT) lds[nn + nt + nm + i] = p.sc.spheres[i];
-    SceneView S;
-    S.nodes = LDS ? lds : p.sc.nodes;
-    S.tris = LDS ? lds + nn : p.sc.tris;
-    S.mats = lds + nn + nt;
-    S.spheres = lds + nn + nt + nm;
-    S.np = N;
-    S.tp = LDS ? T : 0;
-    const int P = p.wf_paths;
-    WfLds L;
-    L.r0 = nn + nt + nm + ns;
-    L.r1 = L.r0 + P;
-    L.r2 = L.r1 + P;
-    L.q0 = L.r2 + P;
-    L.q1 = L.q0 + P;
-    L.q2 = L.q1 + P;
-    L.ring = (unsigned)(L.q2 + P) << 4;
-    L.rmask = (unsigned)p.wf_ring - 1u;
-    L.ctr = L.ring + 3u * (unsigned)p.wf_ring * 2u;
-    // every slot starts fresh (no pixel) in the shade queue, which hands it its first item
-    for (int i = tid; i < 3 * p.wf_ring / 2; i += NT) *(lds_u32*)(size_t)(L.ring + 4u * i) = 0u;
-    if (tid < 16) *wf_ctr(L, tid) = 0u;
-    __syncthreads();
-    for (int sl = tid; sl < P; sl += NT) {
-        wf_st(L.q2, sl, v4f{0.0f, 0.0f, __uint_as_float((kWfFresh | kWfNeedRay) << 8), __uint_as_float(~0u)});
-        *(lds_u16*)(size_t)(L.ring + 2u * ((unsigned)kWfQS * (unsigned)p.wf_ring + sl)) = (unsigned short)(sl + 1);
-    }
-    if (tid == 0) {
-        *wf_ctr(L, 3 * kWfQS) = (unsigned)P;
-        *wf_ctr(L, 3 * kWfQS + 2) = (unsigned)P;
-        *wf_ctr(L, kWfLive) = (unsigned)P;
-    }
-    __syncthreads();
-
-    const int tiles_x = (p.W + 7) >> 3;
-    const unsigned n_groups = (unsigned)((p.n_frames + p.group - 1) / p.group);
-    const unsigned total_ids = (unsigned)tiles_x * (unsigned)((p.rows_local + 7) >> 3) * n_groups * 64u;
-    const int root_skip = p.root_child < 0 ? -1 : p.root_child << (LDS ? 4 : 0);
-
-    // the wave's walkers (w < 0: lane free, slot -1 once its ray is queued)
-    int slot = -1, w = -1;
-    f3 o = mk(0, 0, 0), d = mk(0, 0, 1), rd = mk(0, 0, 0);
-    float t = 0.0f;
-    bool fast = false;
-    unsigned long long idle_t0 = 0;       // watchdog: start of the current idle stretch
-    WfDiag dg;
-#ifdef PT_WF_DIAG
-    unsigned long long dclk = clock64();
-#define WF_CLK(i) do { const unsigned long long c1_ = clock64(); WF_DIAG(i, c1_ - dclk); dclk = c1_; } while (0)
-#else
-#define WF_CLK(i) do { } while (0)
-#endif
-    for (;;) {
-        const unsigned aL = wf_peek(L, 3 * kWfQL + 2), aS = wf_peek(L, 3 * kWfQS + 2);
-        // full batches (all 64 lanes, or none when another wave took them first)
-        if ((int)aL >= p.wf_leaf_min && wf_leaf_batch<LDS>(p, S, L, dg, p.wf_leaf_min >= 64)) { idle_t0 = 0; WF_CLK(8); continue; }
-        if ((int)aS >= p.wf_shade_min &&
-            wf_shade_batch<LDS>(p, S, L, total_ids, n_groups, root_skip, dg, p.wf_shade_min >= 64)) {
-            idle_t0 = 0;
-            WF_CLK(9);
-            continue;
-        }
-        // refill free lanes from the walk queue
-        const unsigned long long freem = __ballot(w < 0);
-        if (freem) {
-            const int s = wf_pop(L, kWfQW, freem, p.wf_err, dg);
-            if (s >= 0) {
-                const v4f a0 = wf_ld(L.r0, s), a1 = wf_ld(L.r1, s), a2 = wf_ld(L.r2, s);
-                o = mk(a0.x, a0.y, a0.z);
-                t = a0.w;
-                d = mk(a1.x, a1.y, a1.z);
-                rd = mk(a2.x, a2.y, a2.z);
-                w = __float_as_int(a2.w);
-                fast = a2.x != 0.0f;
-                slot = s;
-            }
-            WF_DIAG(11, __popcll(__ballot(s >= 0)));
-        }
-        if (__any(w >= 0)) {
-            idle_t0 = 0;
-            if (__all(fast || w < 0)) wf_walk<true, LDS, PADN>(S, o, d, rd, fast, t, p.wf_refill, w, dg);
-            else wf_walk<false, LDS, PADN>(S, o, d, rd, fast, t, p.wf_refill, w, dg);
-            // stopped rays: at a hit leaf (w <= -2) to the leaf queue, walk ended (-1) to shading
-            const bool stopped = (w < 0) & (slot >= 0);
-            if (stopped & (w <= -2)) wf_stw(L.r2, slot, __int_as_float(w));
-            wf_push(L, kWfQL, stopped & (w <= -2), slot);
-            wf_push(L, kWfQS, stopped & (w == -1), slot);
-            if (stopped) slot = -1;
-            WF_CLK(7);
-            continue;
-        }
-        // nothing to walk: drain whatever the queues hold, else wait for the other waves
-        if (aL && wf_leaf_batch<LDS>(p, S, L, dg, false)) { idle_t0 = 0; WF_CLK(8); continue; }
-        if (aS && wf_shade_batch<LDS>(p, S, L, total_ids, n_groups, root_skip, dg, false)) { idle_t0 = 0; WF_CLK(9); continue; }
-        if (wf_peek(L, kWfLive) == 0u) break;
-        // watchdog (100 MHz clock): idle for 2 s while paths are live means a lost path;
-        // give up (the host reports PT_E_HIP) rather than spin forever
-        const unsigned long long now = __builtin_amdgcn_s_memrealtime();
-        if (idle_t0 == 0) idle_t0 = now;
-        else if (now - idle_t0 > 200000000ull) {
-            if (lane_id() == 0) atomicAdd(p.wf_err, 1u);
-            break;
-        }
-        __builtin_amdgcn_s_sleep(2);
-        WF_DIAG(6, 1);
-        WF_CLK(10);
-    }
-#undef WF_CLK
-    dg.flush();
-}
-
 // ACES film tonemap epilogue (screenQuadFrag.c:12-26) -> RGBA8, alpha 255.
 __global__ __launch_bounds__(256) void k_aces(const float4* __restrict__ src, uchar4* __restrict__ dst,
                                               long long n) {
@@ -2360,9 +1218,6 @@ struct pt_ctx {
     int leaf_thresh = 0, shade_thresh = 0, minw = 0, trav_floor = 0, compact_max = 63, pull_batch = 0;
     // frame-split work items (KParams::group): 0 = automatic, n = frames per item
     int group_force = 0;
-    // variant 4 knobs (0 = automatic): path slots per workgroup, refill walker count,
-    // leaf / shade batch minimum
-    int wf_paths = 0, wf_refill = 0, wf_leaf_min = 0, wf_shade_min = 0, wf_threads = 0;
     int n_cu = 0;
     float* d_rgb = nullptr;        // per-(frame, pixel) colours of the frame-split mode
     size_t rgb_bytes = 0;
@@ -2379,7 +1234,6 @@ struct pt_ctx {
     float last_ms = 0.0f;
     unsigned long long last_counts[16] = {0};
     bool count_pending = false;
-    bool wf_check = false;          // a variant-4 launch is pending: check its watchdog word
     std::string err;
 };
 
@@ -2409,6 +1263,13 @@ static int fail(pt_ctx* c, int code, const std::string& msg) {
 // every internal box contains both children's boxes (exact float compares).  A walk that
 // enters a subtree the exact test would skip then leaves it at the same miss link, and any
 // leaf inside has a box within the skipped one, which fails the exact test too.
+// A link field as a node index: finite, integral and in [-1, n_nodes), else -2 (never a
+// valid link; casting NaN or a huge float to int would be undefined behaviour).
+static int link_of(float v, int n_nodes) {
+    if (!(v >= -1.0f && v < (float)n_nodes) || v != (float)(int)v) return -2;
+    return (int)v;
+}
+
 static bool nested_tree(const float* bvh, int n_nodes) {
     if (n_nodes <= 0) return false;
     std::vector<unsigned char> seen(n_nodes, 0);
@@ -2420,12 +1281,16 @@ static bool nested_tree(const float* bvh, int n_nodes) {
         if (x < 0 || x >= n_nodes || seen[x]) return false;
         seen[x] = 1;
         const float* nd = bvh + 12 * (size_t)x;
-        if ((int)nd[11] != after) return false;
-        if (nd[8] > -1.0f) continue;               // leaf: hit == miss (checked by the caller)
-        const int l = (int)nd[10];
-        if (l < 0 || l >= n_nodes) return false;
-        const int r = (int)bvh[12 * (size_t)l + 11];
-        if (r < 0 || r >= n_nodes || r == after) return false;
+        const int hit = link_of(nd[10], n_nodes), miss = link_of(nd[11], n_nodes);
+        if (hit == -2 || miss != after) return false;
+        if (nd[8] > -1.0f) {                       // leaf: its hit link is its miss link
+            if (hit != miss) return false;
+            continue;
+        }
+        const int l = hit;
+        if (l < 0) return false;
+        const int r = link_of(bvh[12 * (size_t)l + 11], n_nodes);
+        if (r < 0 || r == after) return false;
         for (int ch : {l, r}) {
             const float* cb = bvh + 12 * (size_t)ch;
             for (int q = 0; q < 3; q++)
@@ -2539,10 +1404,15 @@ int pt_upload_scene(pt_ctx* c, const float* tris, int n_tris, const float* bvh, 
     for (int i = 0; i < n_nodes; i++) {
         const float* nd = bvh + 12 * (size_t)i;
         bool leaf = nd[8] > -1.0f;
-        int hl = (int)nd[10], ml = (int)nd[11];
-        if (hl < -1 || hl >= n_nodes || ml < -1 || ml >= n_nodes)
+        // the shader's int(float) truncates; values outside (-2, n) -- NaN included -- are
+        // rejected before any cast (a float-to-int cast out of range is undefined)
+        const auto in_open = [](float v, float lo, float hi) { return v > lo && v < hi; };
+        if (!in_open(nd[10], -2.0f, (float)n_nodes) || !in_open(nd[11], -2.0f, (float)n_nodes))
             return fail(c, PT_E_SCENE, "BVH link out of range at node " + std::to_string(i));
+        int hl = (int)nd[10], ml = (int)nd[11];
         if (leaf) {
+            if (!in_open(nd[8], -1.0f, (float)n_tris) || !in_open(nd[9], -1.0f, (float)n_tris))
+                return fail(c, PT_E_SCENE, "leaf triangle index out of range at node " + std::to_string(i));
             int t0 = (int)nd[8], t1 = (int)nd[9];
             if (t0 < 0 || t0 >= n_tris || t1 < 0 || t1 >= n_tris)
                 return fail(c, PT_E_SCENE, "leaf triangle index out of range at node " + std::to_string(i));
@@ -2572,12 +1442,12 @@ int pt_upload_scene(pt_ctx* c, const float* tris, int n_tris, const float* bvh, 
         }
     }
     for (int i = 0; i < n_tris; i++) {
-        int m = (int)tris[16 * (size_t)i + 12];
-        if (m < 0 || m >= n_mats) return fail(c, PT_E_SCENE, "triangle material index out of range");
+        const float fm = tris[16 * (size_t)i + 12];
+        if (!(fm > -1.0f && fm < (float)n_mats)) return fail(c, PT_E_SCENE, "triangle material index out of range");
     }
     for (int i = 0; i < n_spheres; i++) {
-        int m = (int)spheres[8 * (size_t)i + 4];
-        if (m < 0 || m >= n_mats) return fail(c, PT_E_SCENE, "sphere material index out of range");
+        const float fm = spheres[8 * (size_t)i + 4];
+        if (!(fm > -1.0f && fm < (float)n_mats)) return fail(c, PT_E_SCENE, "sphere material index out of range");
     }
     // --- device node numbering: the first kTopNodes nodes in breadth-first order of the walk
     // links from the root (the nodes nearly every walk passes: the global-memory walk keeps
@@ -2644,8 +1514,6 @@ int pt_upload_scene(pt_ctx* c, const float* tris, int n_tris, const float* bvh, 
             b = (int)nd[11];
         }
         if (b >= 0) b = pos[b];
-        if (leaf_slot[i] >= 0)     // global-memory walks of variant 4: the leaf's next-right
-            std::memcpy(&dt[8 * (size_t)leaf_slot[i] + 3].w, &b, 4);
         float fa, fb;
         std::memcpy(&fa, &a, 4);
         std::memcpy(&fb, &b, 4);
@@ -2832,9 +1700,9 @@ int pt_set_counting(pt_ctx* c, int enable) {
 
 int pt_set_kernel(pt_ctx* c, int variant) {
     if (!c) return PT_E_ARG;
-    if (variant < 0 || variant > 4)
-        return fail(c, PT_E_ARG, "unknown kernel variant (0 state machine, 1 tiled, 2 while-while, 3 state machine / "
-                                 "global scene, 4 wavefront queues)");
+    if (variant != 0 && variant != 3)
+        return fail(c, PT_E_ARG, "unknown kernel variant (0 state machine, 3 state machine with the scene kept in "
+                                 "global memory)");
     c->variant = variant;
     drop_graph(c);
     return PT_OK;
@@ -2857,20 +1725,6 @@ int pt_set_tuning(pt_ctx* c, int key, int value) {
     if (key == 15) {
         if (value != 0 && value != 1) return fail(c, PT_E_ARG, "culling walk: 0 = automatic, 1 = off");
         c->cons_off = value;
-        drop_graph(c);
-        return PT_OK;
-    }
-    if (key == 14) {
-        if (value != 0 && value != 512 && value != 768 && value != 896 && value != 1024)
-            return fail(c, PT_E_ARG, "wavefront workgroup size must be 512, 768, 896 or 1024 (0 = automatic)");
-        c->wf_threads = value;
-        drop_graph(c);
-        return PT_OK;
-    }
-    if (key >= 10 && key <= 13) {
-        if (value < 0 || (key == 10 && value > 1536) || (key > 10 && value > 64))
-            return fail(c, PT_E_ARG, "wavefront knob out of range");
-        (key == 10 ? c->wf_paths : key == 11 ? c->wf_refill : key == 12 ? c->wf_leaf_min : c->wf_shade_min) = value;
         drop_graph(c);
         return PT_OK;
     }
@@ -2927,7 +1781,7 @@ int pt_set_tuning(pt_ctx* c, int key, int value) {
 // accumulates in registers).  The counting build follows the same plan: with whole-pixel
 // items a 1080p/8 share of a 1024-frame launch would run each lane through 1024 frames
 // in sequence (minutes).
-// Whether the state-machine kernel (variants 0 and 4's fallback) stages the scene in LDS:
+// Whether the state-machine kernel stages the scene in LDS:
 // up to kLdsSceneSmall always; up to kLdsSceneMax when wide workgroups share the copy
 // (lds_threads' configuration).  Variant 3 forces the global-memory walk.
 static bool lds_staged(const pt_ctx* c) {
@@ -2937,7 +1791,6 @@ static bool lds_staged(const pt_ctx* c) {
 }
 
 static int plan_group(const pt_ctx* c, int n_frames) {
-    if (c->variant != 0 && c->variant != 3 && c->variant != 4) return n_frames;
     if (c->group_force > 0) return std::min(c->group_force, n_frames);
     const int waves = c->minw ? c->minw : 6;
     const double lanes = (double)c->n_cu * 4.0 * waves * 64.0;
@@ -2962,9 +1815,10 @@ constexpr int kShortLaunch = 16;
 #endif
 constexpr int kOrderEvery = PT_ORDER_EVERY;   // short launches per tile-order sort (enqueue_render)
 constexpr int kOrderFirst = 8;                // ... and before the first sort after an upload
+constexpr int kProbeFrames = 2, kProbeMin = 64;  // cold long renders: a sorted order after 2 frames
 static bool split_mode(const pt_ctx* c, int n_frames, int group) {
     if (group < n_frames) return true;
-    return c->group_force == 0 && (c->variant == 0 || c->variant == 3) && n_frames <= kShortLaunch;
+    return c->group_force == 0 && n_frames <= kShortLaunch;
 }
 
 // Grows the frame-split scratch to n_frames frame planes.  Earlier launches on the stream may
@@ -2983,33 +1837,6 @@ static int ensure_rgb(pt_ctx* c, int n_frames) {
     return PT_OK;
 }
 
-// Variant 4 (wavefront queues) runs when the scene is staged in LDS with room beside it for
-// the path slots (96 B each), raysPerPixel is 1, nothing is counted and the packed path
-// counters fit (bounce < 256, frames per launch < 2^16); it always stores per-frame colours.
-// Otherwise variant 4 falls back to the state-machine kernel (variant 0).  Returns the path
-// slots per workgroup, 0 when variant 4 does not run.
-static int wf_threads(const pt_ctx* c) { return c->wf_threads ? c->wf_threads : 1024; }
-// LDS bytes of variant 4's scene part: an LDS-staged scene as variant 0 stages it; for a
-// global-memory scene the top nodes plus materials and spheres (-1: these do not fit).
-static long long wf_scene_bytes(const pt_ctx* c) {
-    if (c->lds_bytes <= kLdsSceneSmall) return (long long)c->lds_bytes;
-    const long long shade = (3LL * c->n_mats + 2LL * c->n_spheres) * 16;
-    if (shade > 4096) return -1;
-    return (long long)c->n_top * 32 + shade;
-}
-static int wf_paths(const pt_ctx* c, int n_frames) {
-    if (c->variant != 4 || c->counting || c->cfg.rays_per_pixel != 1 || c->cfg.max_bounce > 250 || n_frames > 65535)
-        return 0;
-    const long long scene = wf_scene_bytes(c);
-    if (scene < 0) return 0;
-    const int per_cu = wf_threads(c) <= 512 ? 4 : (wf_threads(c) < 1024 ? 2 : 1);   // workgroups per CU
-    // 96 B of records per path slot plus 3 ring entries (2 B, rings of at most 2x the slots)
-    const long long room = 160 * 1024 / per_cu - scene - 64;
-    const int fit = (int)std::min<long long>(room / (96 + 12), 1536);
-    const int P = c->wf_paths ? std::min(c->wf_paths, fit) : fit;
-    return P >= 64 ? P : 0;
-}
-
 // Queue ids are 32-bit: a launch's items * 64 plus what the resident waves can reserve past
 // the end (each wave pulls at most 64 ids, twice after the queue ran dry) stay below 2^32.
 constexpr unsigned long long kIdLimit = (1ull << 32) - (1ull << 24);
@@ -3024,11 +1851,13 @@ static int launch_frames(const pt_ctx* c, int n_frames) {
     int n = n_frames;
     for (;;) {
         const int g = plan_group(c, n);
-        if (!split_mode(c, n, g) && !wf_paths(c, n)) return n;    // register mode: no scratch, one group
-        const unsigned long long by_budget = c->scratch_budget / (px * 12ull);
+        if (!split_mode(c, n, g)) return n;    // register mode: no scratch, one group
+        // one frame per launch always runs, even when its scratch exceeds the budget (so n
+        // strictly decreases to at most 1: the loop ends)
+        const unsigned long long by_budget = std::max(1ull, c->scratch_budget / (px * 12ull));
         const unsigned long long ng = (unsigned long long)((n + g - 1) / g);
         const unsigned long long by_ids = (kIdLimit / tiles64) * (unsigned long long)g;
-        if ((unsigned long long)n <= by_budget && ng * tiles64 < kIdLimit) return n;
+        if (((unsigned long long)n <= by_budget && ng * tiles64 < kIdLimit) || n == 1) return n;
         const unsigned long long m = std::min<unsigned long long>({(unsigned long long)n - 1, by_budget, by_ids});
         n = (int)std::max<unsigned long long>(m, 1ull);
     }
@@ -3067,7 +1896,7 @@ static int lds_threads(const pt_ctx* c, size_t lds) {
 // Enqueues one render launch (work-queue reset + kernel) on the context stream.  With
 // `frame_dev` the frame range is read on the device (progressive graph replay).
 static int enqueue_render(pt_ctx* c, int frame_first, int n_frames, int acc_first, const int* frame_dev,
-                          int frame_offset) {
+                          int frame_offset, bool force_sort = false) {
     KParams p;
     std::memset(&p, 0, sizeof(p));
     p.sc.nodes = c->d_nodes;
@@ -3139,8 +1968,7 @@ static int enqueue_render(pt_ctx* c, int frame_first, int n_frames, int acc_firs
         const unsigned long long items = (unsigned long long)c->n_tiles * ng;
         p.grp_magic = (ng > 1 && items * ng < (1ull << 32)) ? (unsigned)(((1ull << 32) + ng - 1) / ng) : 0u;
     }
-    const int wfP = wf_paths(c, n_frames);
-    if (split_mode(c, n_frames, p.group) || wfP) {
+    if (split_mode(c, n_frames, p.group)) {
         int rc = ensure_rgb(c, n_frames);
         if (rc) return rc;
         p.rgb = c->d_rgb;
@@ -3148,50 +1976,11 @@ static int enqueue_render(pt_ctx* c, int frame_first, int n_frames, int acc_firs
     p.tile_perm = c->d_tile_perm;
     p.tile_cost = (c->adaptive && !c->counting) ? c->d_tile_cost : nullptr;
     if (c->rows_local == 0) return PT_OK;
-    // variants: 0 state-machine persistent (default), 1 one-lane-per-pixel tiles,
-    // 2 while-while persistent, 3 = 0 with the scene forced to stay in global memory
-    const int variant = c->variant == 4 ? 0 : c->variant;   // variant 4's fallback is variant 0
-    bool use_lds = (variant == 0 && lds_staged(c)) || (variant == 2 && c->lds_bytes <= kLdsSceneSmall);
-    if (variant != 1 && !wfP) HIPCHK(c, hipMemsetAsync(c->d_work, 0, sizeof(unsigned), c->stream));
-    if (wfP) {
-        HIPCHK(c, hipMemsetAsync(c->d_work, 0, 8 * sizeof(unsigned), c->stream));
-        c->wf_check = true;
-        // one 1024-thread workgroup per CU (16 waves share the scene copy and wfP path
-        // slots); no more workgroups than the pixel-frame items fill
-        p.wf_paths = wfP;
-        p.wf_ring = 64;
-        while (p.wf_ring < wfP) p.wf_ring <<= 1;
-        p.wf_err = c->d_work + 4;            // reset with the queue counter below
-        // keysweep: LDS scenes 16 (+4% over 40), global-memory scenes 40 (+15% over 16)
-        p.wf_refill = c->wf_refill ? c->wf_refill : (c->lds_bytes <= kLdsSceneSmall ? 16 : 40);
-        p.wf_leaf_min = c->wf_leaf_min ? c->wf_leaf_min : 64;
-        p.wf_shade_min = c->wf_shade_min ? c->wf_shade_min : 64;
-        const size_t lds = (size_t)wf_scene_bytes(c) + 96 * (size_t)wfP + 3 * (size_t)p.wf_ring * 2 + 64;
-        const bool wl = c->lds_bytes <= kLdsSceneSmall;    // LDS-staged scene (else global)
-        const unsigned long long ids = (unsigned long long)c->n_tiles * 64ull *
-                                       (unsigned long long)((n_frames + p.group - 1) / p.group);
-        const int nt = wf_threads(c);
-        const unsigned per_cu = nt <= 512 ? 4u : (nt < 1024 ? 2u : 1u);
-        const unsigned grid = (unsigned)std::min<unsigned long long>(
-            (unsigned long long)c->n_cu * per_cu, std::max(1ull, (ids + wfP - 1) / (unsigned long long)wfP));
-#define PT_WF(NT)                                                                                             \
-    if (!wl) hipLaunchKernelGGL((k_render_wf<false, false, NT, NT / 64 * (NT <= 512 ? 4 : (NT < 1024 ? 2 : 1)) / 4>), dim3(grid), dim3(NT), lds, c->stream, p); \
-    else if (c->walk_np == kPadNodes) hipLaunchKernelGGL((k_render_wf<true, true, NT, NT / 64 * (NT <= 512 ? 4 : (NT < 1024 ? 2 : 1)) / 4>), dim3(grid), dim3(NT), lds, c->stream, p); \
-    else hipLaunchKernelGGL((k_render_wf<true, false, NT, NT / 64 * (NT <= 512 ? 4 : (NT < 1024 ? 2 : 1)) / 4>), dim3(grid), dim3(NT), lds, c->stream, p);
-        if (nt == 512) { PT_WF(512) }
-        else if (nt == 768) { PT_WF(768) }
-        else if (nt == 896) { PT_WF(896) }
-        else { PT_WF(1024) }
-#undef PT_WF
-        long long px = (long long)c->rows_local * p.W;
-        hipLaunchKernelGGL(k_accum_frames, dim3((unsigned)((px + 255) / 256)), dim3(256), 0, c->stream, p);
-    } else if (variant == 1) {
-        dim3 grid((p.W + 15) / 16, (c->rows_local + 15) / 16);
-        if (c->counting)
-            hipLaunchKernelGGL(k_render_tiled<true>, grid, dim3(256), 0, c->stream, p);
-        else
-            hipLaunchKernelGGL(k_render_tiled<false>, grid, dim3(256), 0, c->stream, p);
-    } else {
+    // variants: 0 state machine (default), 3 = 0 with the scene forced to stay in global memory
+    const int variant = c->variant;
+    const bool use_lds = variant == 0 && lds_staged(c);
+    HIPCHK(c, hipMemsetAsync(c->d_work, 0, sizeof(unsigned), c->stream));
+    {
         // persistent grid: enough resident waves to fill every SIMD; surplus blocks find the
         // queue empty and exit.  Never more blocks than 8x8 tiles (64 lanes per tile).
         size_t lds = use_lds ? ((PT_WALK_SINKS && p.cons_walk) ? c->lds_bytes_sk : c->lds_bytes) : 0;
@@ -3202,9 +1991,6 @@ static int enqueue_render(pt_ctx* c, int frame_first, int n_frames, int acc_firs
         unsigned blocks = std::min<unsigned>(c->persist_blocks * 256u / (unsigned)nt,
                                              std::max(1u, (items + wpb - 1) / wpb));
         dim3 grid(blocks);
-#define PT_LAUNCH(K, L, MW)                                                                                   \
-    if (c->counting) hipLaunchKernelGGL((K<true, L, MW>), grid, dim3(256), L ? lds : 0, c->stream, p);        \
-    else hipLaunchKernelGGL((K<false, L, MW>), grid, dim3(256), L ? lds : 0, c->stream, p);
         // occupancy: 7 waves/SIMD for LDS scenes (72 VGPRs, a few spilled: +0.8% on C2 over
         // 6, which was +5% over 5; 8 spills 20+ and loses 7%), 6 for global-memory scenes (7
         // leaves fewer top nodes per block in LDS: -6% on the C3 stand-in)
@@ -3236,18 +2022,14 @@ static int enqueue_render(pt_ctx* c, int frame_first, int n_frames, int acc_firs
             else if (nt == 768) { PT_LAUNCH_WIDE(768, 6) }
             else { PT_LAUNCH_WIDE(1024, 4) }
 #undef PT_LAUNCH_WIDE
-        } else if (variant == 0 || variant == 3) {
+        } else {
             bool multi = p.rpp > 1;
             if (use_lds && multi) { PT_LAUNCH_SM(true, true) }
             else if (use_lds) { PT_LAUNCH_SM(true, false) }
             else if (multi) { PT_LAUNCH_SM(false, true) }
             else { PT_LAUNCH_SM(false, false) }
 #undef PT_LAUNCH_SM
-        } else {
-            if (use_lds) { PT_LAUNCH(k_render_wave, true, 1) }
-            else { PT_LAUNCH(k_render_wave, false, 1) }
         }
-#undef PT_LAUNCH
         if (p.rgb) {
             long long px = (long long)c->rows_local * p.W;
             hipLaunchKernelGGL(k_accum_frames, dim3((unsigned)((px + 255) / 256)), dim3(256), 0, c->stream, p);
@@ -3260,7 +2042,7 @@ static int enqueue_render(pt_ctx* c, int frame_first, int n_frames, int acc_firs
     // (same-process A/B of one-frame launches, against sorting every launch: every 4th
     // +6%, 8th +8.4%, 16th +9.8%, 64th +10.7%).  Captured graphs (frame_dev) sort every replay.
     if (p.tile_cost && c->n_tiles > 1 &&
-        (frame_dev || n_frames > kShortLaunch ||
+        (frame_dev || force_sort || n_frames > kShortLaunch ||
          ++c->order_skip >= (c->order_sorted ? kOrderEvery : kOrderFirst))) {
         c->order_skip = 0;
         c->order_sorted = true;
@@ -3290,6 +2072,17 @@ static int take_events(pt_ctx* c, hipEvent_t ev[2]) {
 // running mean (accumulate = 1), so the image is that of n_frames single dispatches.
 static int enqueue_frames(pt_ctx* c, int frame_first, int n_frames, int acc_first, const int* frame_dev,
                           int frame_offset) {
+    // A long render on a context whose tile order was never sorted (the first render after an
+    // upload) would run in raster order.  Its first kProbeFrames frames go first as a short
+    // launch whose tile costs are sorted at once, so the remaining frames already run most-
+    // expensive-tile-first; the continuation accumulates, so the image is unchanged.
+    if (!frame_dev && c->adaptive && !c->counting && !c->order_sorted && n_frames >= kProbeMin) {
+        int rc = enqueue_render(c, frame_first, kProbeFrames, acc_first, nullptr, 0, true);
+        if (rc) return rc;
+        frame_first += kProbeFrames;
+        n_frames -= kProbeFrames;
+        acc_first = 1;
+    }
     const int step = launch_frames(c, n_frames);
     for (int done = 0; done < n_frames; done += step) {
         const int n = std::min(step, n_frames - done);
@@ -3392,7 +2185,6 @@ int pt_progressive_run(pt_ctx* c, int replays) {
     c->ev_pending.emplace_back(ev[0], ev[1]);
     HIPCHK(c, hipEventRecord(ev[0], c->stream));
     for (int r = 0; r < replays; r++) HIPCHK(c, hipGraphLaunch(c->graph_exec, c->stream));
-    if (c->variant == 4) c->wf_check = true;
     HIPCHK(c, hipEventRecord(ev[1], c->stream));
     return PT_OK;
 }
@@ -3411,12 +2203,6 @@ int pt_sync(pt_ctx* c) {
         c->ev_free.push_back(pr.second);
     }
     c->ev_pending.clear();
-    if (c->wf_check) {
-        unsigned trips = 0;
-        HIPCHK(c, hipMemcpy(&trips, c->d_work + 4, sizeof(unsigned), hipMemcpyDeviceToHost));
-        c->wf_check = false;
-        if (trips) return fail(c, PT_E_HIP, "wavefront kernel watchdog tripped (" + std::to_string(trips) + " waves)");
-    }
     if (c->count_pending) {
         HIPCHK(c, hipMemcpy(c->last_counts, c->d_counters, 16 * sizeof(unsigned long long), hipMemcpyDeviceToHost));
         c->count_pending = false;
@@ -3513,17 +2299,6 @@ extern "C" int pt_debug_phase_clock(unsigned long long out[8], int reset) {
 }
 #endif
 
-#ifdef PT_WF_DIAG
-extern "C" int pt_debug_wf_diag(unsigned long long out[16], int reset) {
-    if (hipDeviceSynchronize() != hipSuccess) return -1;
-    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_wf_diag), sizeof(unsigned long long) * 16) != hipSuccess) return -1;
-    if (reset) {
-        unsigned long long z[16] = {0};
-        if (hipMemcpyToSymbol(HIP_SYMBOL(g_wf_diag), z, sizeof(z)) != hipSuccess) return -1;
-    }
-    return 0;
-}
-#endif
 
 int pt_stats_ex(pt_ctx* c, unsigned long long out[16]) {
     if (!c || !out) return PT_E_ARG;

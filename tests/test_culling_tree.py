@@ -53,3 +53,24 @@ def test_nan_bounds_disqualify(cornell_scene):
     n = nodes_of(cornell_scene)
     n[int(n[0, 10]), 1] = np.nan
     assert not H.bvh_culling_ok(n)
+
+
+def test_bad_link_floats_disqualify(cornell_scene):
+    """Link fields that are NaN, huge, fractional or out of range are refused before any
+    float-to-int cast: the tree no longer qualifies."""
+    for bad in (np.nan, 1e30, -1e30, 2.5, 1e9):
+        n = nodes_of(cornell_scene)
+        n[int(n[0, 10]), 11] = bad
+        assert not H.bvh_culling_ok(n), bad
+        n = nodes_of(cornell_scene)
+        n[0, 10] = bad
+        assert not H.bvh_culling_ok(n), bad
+
+
+def test_leaf_with_distinct_hit_and_miss_disqualifies(cornell_scene):
+    """A leaf's hit link must equal its miss link (both next-right, bvh.h:84-98); the public
+    check no longer relies on its caller for that."""
+    n = nodes_of(cornell_scene)
+    leaf = int(np.argmax(n[:, 8] > -1.0))
+    n[leaf, 10] = 0 if n[leaf, 11] != 0 else 1
+    assert not H.bvh_culling_ok(n)

@@ -114,3 +114,24 @@ def test_two_devices_one_process(cornell_scene):
         assert np.array_equal(pt.read_rgba8(), O.aces_rgba8(want))
     for pt in pts:
         pt.close()
+
+
+def test_budget_below_one_frame_still_renders(cornell_scene):
+    """A 1 MiB scratch budget at 1920x1080 is smaller than one frame's split scratch (24.9 MB):
+    short renders must run one frame per launch (over budget) and return, not spin on the
+    host.  Checked at sampled pixels against the oracle."""
+    W, Hh = 1920, 1080
+    pt = H.PathTracer(W, Hh, max_bounce=4)
+    pt.set_tuning(scratch_mib=1)
+    pt.upload(cornell_scene)
+    pt.render(1, 1, 0)
+    pt.render(2, 2, 1)
+    pt.progressive_setup(frames_per_launch=1, launches_per_replay=2)
+    pt.progressive_reset(4)
+    pt.progressive_run(replays=1)
+    got = pt.read_rgba32f()
+    pt.close()
+    rng = np.random.default_rng(2)
+    xs, ys = rng.integers(0, W, 2000), rng.integers(0, Hh, 2000)
+    want = O.render_pixels(cornell_scene, W, Hh, xs, ys, max_bounce=4, n_frames=5)
+    assert_bitwise(got[ys, xs], want, "sub-frame budget")

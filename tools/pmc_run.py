@@ -23,8 +23,8 @@ sb = pt_host.setupBuffers(*pt_scenes.write_scene(a.scene, os.path.join(REPO, "sc
 pt = pt_host.PathTracer(a.width, a.height, max_bounce=8)
 pt.set_kernel(a.variant)
 pt.upload(sb)
-pt.render(1, a.chunk, 0)
-for i in range(a.launches):
-    pt.render(1 + a.chunk * (i + 1), a.chunk, 1)
+# the bench's step: frames 1..chunk from accumulate = 0, re-rendered (warm-up launch first)
+for i in range(a.launches + 1):
+    pt.render(1, a.chunk, 0)
 pt.close()
 print("pmc workload done")

@@ -56,7 +56,11 @@ def main():
         if not os.path.isdir(d) or not os.path.exists(os.path.join(d, "run_counter_collection.csv")):
             continue
         launches = load(d)
-        for ctr, ms in (launches[1:] or launches):     # drop the warm-up launch when possible
+        # full-size launches only (a cold first render starts with a 2-frame probe launch),
+        # then drop the warm-up render when possible
+        top = max(sum(ms.values()) for _, ms in launches)
+        launches = [(ctr, ms) for ctr, ms in launches if sum(ms.values()) >= 0.5 * top]
+        for ctr, ms in (launches[1:] or launches):
             for cn, v in ctr.items():
                 per[cn].append(v)
             per["launch_ms_" + name].append(sum(ms.values()))
@@ -76,6 +80,8 @@ def main():
         cycles = avg["GRBM_GUI_ACTIVE"] / 8.0
         out["valu_busy_frac"] = 2.0 * avg["SQ_INSTS_VALU"] / (1024.0 * cycles)
         out["clock_ghz"] = cycles / (avg.get("launch_ms_sq2", avg.get("launch_ms_sq1", 1.0)) * 1e6)
+        out["valu_instr_per_launch"] = avg["SQ_INSTS_VALU"]
+        out["source"] = "profiles/%s_pmc.json (rocprofv3 --pmc passes of tools/pmc_run.py, same workload)" % tag
     if "SQ_WAVE_CYCLES" in avg and "SQ_WAIT_ANY" in avg:
         tot = avg["SQ_WAVE_CYCLES"]
         out["wave_cycle_split"] = {k: avg[k] / tot for k in ("SQ_ACTIVE_INST_ANY", "SQ_WAIT_INST_ANY", "SQ_WAIT_ANY") if k in avg}

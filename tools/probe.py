@@ -1,6 +1,6 @@
 """Quick A/B of kernel variants / launch shapes on one GPU (interleaved, one process).
 
-python tools/probe.py --spp 64 --variants 0,1,2 --chunks 16,64 --rounds 2
+python tools/probe.py --spp 64 --variants 0,3 --chunks 16,64 --rounds 2
 Prints Mrays/s and kernel ms per configuration; segment counts come from a counting pass.
 """
 import argparse
@@ -35,7 +35,7 @@ def phase_clock(segments):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--spp", type=int, default=64)
-    ap.add_argument("--variants", default="0,1,2")
+    ap.add_argument("--variants", default="0")
     ap.add_argument("--chunks", default="64")
     ap.add_argument("--rounds", type=int, default=2)
     ap.add_argument("--scene", default="cornell")
