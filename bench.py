@@ -137,13 +137,14 @@ def main():
         if distributed:
             dist.barrier()
 
+    # the scene is generated, parsed and its BVH built once, on rank 0, then broadcast
+    # (pt_dist.broadcast_scene; RCCL for nccl) -- every rank renders the same arrays
     scene_dir = os.path.join(REPO, "scenes")
+    sb = None
     if rank == 0:
-        obj, mtl = pt_scenes.write_scene(scene, scene_dir)
-    barrier()
-    obj = os.path.join(scene_dir, "%sobj.txt" % scene)
-    mtl = os.path.join(scene_dir, "%smtl.txt" % scene)
-    sb = pt_host.setupBuffers(obj, mtl)
+        sb = pt_host.setupBuffers(*pt_scenes.write_scene(scene, scene_dir))
+    if distributed:
+        sb = pt_dist.broadcast_scene(sb, device="cuda" if args.dist_backend == "nccl" else "cpu")
     cold_ms = None
     if not args.no_cold and graph_launches == 0:
         # cold first render: a fresh context right after pt_upload_scene (raster tile order

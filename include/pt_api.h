@@ -93,6 +93,8 @@ int pt_progressive_run(pt_ctx* ctx, int replays);
 
 /* Local rows owned by this context: rows y = rank + k*world, k < rows_local. */
 int pt_rows(const pt_ctx* ctx, int* rows_local, int* row0, int* row_stride);
+/* The context's configuration as created (display_mode as last set). */
+int pt_get_config(const pt_ctx* ctx, pt_config* out);
 
 /* Copies the local accumulation rows (rows_local * width * 4 floats, local row 0 =
  * image row `rank`, image row 0 = bottom). */

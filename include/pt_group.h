@@ -1,0 +1,61 @@
+/* pt_group.h -- one process driving an image split over several contexts:
+ * a scene broadcast and the frame gather over RCCL (xGMI between the MI355X devices).
+ *
+ * The reference renders on one GL context: glDispatchCompute + glMemoryBarrier
+ * (ogl_path_trace.h:183-186) and a textured-quad blit of the one image (:189-192).  Split
+ * across G contexts (pt_config rank r of world G owns rows y = r, r + G, ...), the image is
+ * assembled here:
+ *   pt_group_create        one RCCL communicator over the contexts' distinct devices
+ *                          (ncclCommInitAll); several contexts may share a device
+ *   pt_group_upload_scene  pt_upload_scene's validation and layout transposition run once,
+ *                          on the first context; its device scene is broadcast (ncclBroadcast)
+ *                          to one context per device and copied on-device to the rest
+ *   pt_group_gather_rgba32f every context's rows are gathered on the first context's device
+ *                          (ncclGather of padded row blocks) and interleaved there by a
+ *                          device kernel into the full RGBA32F frame, row 0 = bottom; the
+ *                          result goes to host memory or stays in device memory
+ * The gather waits for every context's stream (stream-ordered, no host round trip in
+ * between) and returns once the frame is in `dst`.  The assembled frame is bit-identical to
+ * a single context's render: each pixel's RNG depends only on (x, y, frame)
+ * (computeShader.c:514-515).  Return 0 or a negative PT_E* code; pt_group_last_error explains.
+ */
+#ifndef PT_GROUP_H
+#define PT_GROUP_H
+
+#include <stddef.h>
+
+#include "pt_api.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define PT_E_RCCL (-7)     /* RCCL error (communicator setup or a collective) */
+
+typedef struct pt_group pt_group;
+
+/* ctxs[0..n): contexts of one image (equal width, height and world = n, ranks 0..n-1 in any
+ * order).  The frame is assembled on ctxs[0]'s device.  The contexts must outlive the group. */
+int pt_group_create(pt_ctx* const* ctxs, int n, pt_group** out);
+void pt_group_destroy(pt_group* g);
+const char* pt_group_last_error(const pt_group* g);
+
+/* pt_upload_scene for every context of the group (same arguments and checks). */
+int pt_group_upload_scene(pt_group* g, const float* tris, int n_tris, const float* bvh, int n_nodes,
+                          const float* mats, int n_mats, const float* spheres, int n_spheres);
+
+/* Full frame (height * width * 4 floats = `bytes` or more).  dst_on_device != 0: dst is device
+ * memory on ctxs[0]'s device; else host memory. */
+int pt_group_gather_rgba32f(pt_group* g, float* dst, size_t bytes, int dst_on_device);
+
+/* Device time of the last gather (ms, from the first pack copy to the interleaved frame on the
+ * root device, HIP events) and the bytes each device sent. */
+int pt_group_stats(const pt_group* g, double* gather_ms, size_t* bytes_per_device);
+
+/* One-shot form: create a group, gather, destroy (sets up a communicator on every call). */
+int pt_gather_rgba32f(pt_ctx* const* ctxs, int n, float* dst, size_t bytes, int dst_on_device);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* PT_GROUP_H */

@@ -5,11 +5,13 @@
 // SURVEY.md §0.1); this driver honours the README's intent (readme.md:8-9): the .obj and
 // .mtl come from the command line.  Frames f = 1..spp are rendered with accumulate = 0
 // on frame 1 (ogl_path_trace.h:160-204 after a reset), fused `chunk` frames per launch,
-// optionally row-split across several GPUs of this node (one context per device).
+// optionally row-split across several GPUs of this node: --ranks R contexts (rank r on device
+// r mod G), the scene validated once and broadcast, the frame gathered over RCCL (pt_group.h).
 //
 // Output: RGBA32F accumulation as PFM (row 0 = bottom, like the GL texture) and the
 // ACES-tonemapped RGBA8 view as binary PPM (screenQuadFrag.c).
 #include "../../include/pt_api.h"
+#include "../../include/pt_group.h"
 #include "../../include/pt_scene.h"
 #include "../../include/pt_viewer.h"
 
@@ -25,7 +27,7 @@
 static void usage() {
     std::fprintf(stderr,
                  "usage: ptrace <scene.obj> <scene.mtl | -> [--width W] [--height H] [--spp S] [--chunk C]\n"
-                 "              [--bounces B] [--mode 1..4] [--gpus G] [--pfm out.pfm] [--ppm out.ppm]\n"
+                 "              [--bounces B] [--mode 1..4] [--gpus G] [--ranks R] [--pfm out.pfm] [--ppm out.ppm]\n"
                  "              [--camera px py pz dx dy dz] [--robust] [--events script.txt]\n"
                  "  --robust  general Wavefront ingest (v/vt/vn corners, polygons, negative indices,\n"
                  "            free-form MTL; '-' as the MTL uses the OBJ's mtllib)\n"
@@ -38,8 +40,12 @@ static void usage() {
                  "                                 ACTION = press | release | repeat\n"
                  "              cursor X Y         cursor callback\n"
                  "            '#' starts a comment; the loop ends early once esc was pressed\n"
+                 "  --gpus G        devices 0..G-1 of this node\n"
+                 "  --ranks R       row-split contexts (default G; rank r renders rows r, r+R, ... on device\n"
+                 "                  r mod G); the frame is gathered over RCCL on device 0\n"
                  "  --checkpoint F  after rendering, save the RGBA32F accumulation and the next frame\n"
-                 "                  number (text header 'PTCK1 W H next_frame', then W*H*4 floats)\n"
+                 "                  number (text header 'PTCK2 W H next_frame bounces mode tris nodes' + the\n"
+                 "                  camera's 6 floats, then W*H*4 floats)\n"
                  "  --resume F      continue a saved accumulation: frames next_frame.. with accumulate = 1,\n"
                  "                  the same image as one uninterrupted run\n"
                  "  --json          print a JSON summary line\n"
@@ -48,23 +54,35 @@ static void usage() {
 
 // Checkpoint of a progressive render (SURVEY.md §5 checkpoint / resume): the running mean
 // (computeShader.c:548-551) only needs the accumulation image and the next frame number.
-static bool save_checkpoint(const std::string& path, int W, int H, int next_frame, const std::vector<float>& img) {
+// The header also records what the running mean depends on besides the image -- bounces,
+// display mode, the scene's triangle and node counts and the camera -- and --resume refuses a
+// checkpoint that does not match them (a silent blend of two different renders otherwise).
+struct CkptKey {
+    int bounces, mode, tris, nodes;
+    float cam[6];
+};
+
+static bool save_checkpoint(const std::string& path, int W, int H, int next_frame, const CkptKey& key,
+                            const std::vector<float>& img) {
     FILE* f = std::fopen(path.c_str(), "wb");
     if (!f) return false;
-    std::fprintf(f, "PTCK1 %d %d %d\n", W, H, next_frame);
+    std::fprintf(f, "PTCK2 %d %d %d %d %d %d %d %.9g %.9g %.9g %.9g %.9g %.9g\n", W, H, next_frame, key.bounces,
+                 key.mode, key.tris, key.nodes, key.cam[0], key.cam[1], key.cam[2], key.cam[3], key.cam[4], key.cam[5]);
     const bool ok = std::fwrite(img.data(), 4, img.size(), f) == img.size();
     return std::fclose(f) == 0 && ok;
 }
 
-static bool load_checkpoint(const std::string& path, int W, int H, int& next_frame, std::vector<float>& img,
-                            std::string& err) {
+static bool load_checkpoint(const std::string& path, int W, int H, int& next_frame, CkptKey& key,
+                            std::vector<float>& img, std::string& err) {
     FILE* f = std::fopen(path.c_str(), "rb");
     if (!f) { err = "cannot open " + path; return false; }
     int w = 0, h = 0, nf = 0;
     char magic[8] = {0};
-    bool ok = std::fscanf(f, "%5s %d %d %d", magic, &w, &h, &nf) == 4 && std::string(magic) == "PTCK1" &&
-              std::fgetc(f) == '\n';
-    if (!ok) err = path + ": not a PTCK1 checkpoint";
+    bool ok = std::fscanf(f, "%5s %d %d %d %d %d %d %d %g %g %g %g %g %g", magic, &w, &h, &nf, &key.bounces, &key.mode,
+                          &key.tris, &key.nodes, &key.cam[0], &key.cam[1], &key.cam[2], &key.cam[3], &key.cam[4],
+                          &key.cam[5]) == 14 &&
+              std::string(magic) == "PTCK2" && std::fgetc(f) == '\n';
+    if (!ok) err = path + ": not a PTCK2 checkpoint";
     else if (w != W || h != H) { ok = false; err = path + ": checkpoint is " + std::to_string(w) + "x" + std::to_string(h); }
     else if (nf < 1) { ok = false; err = path + ": bad next frame"; }
     if (ok) {
@@ -149,7 +167,7 @@ int main(int argc, char** argv) {
     if (argc < 3) { usage(); return 2; }
     const char* obj = argv[1];
     const char* mtl = argv[2];
-    int W = 1000, H = 800, spp = 64, chunk = 16, bounces = 5, mode = 1, gpus = 1;   // ogl_path_trace.h:45-46
+    int W = 1000, H = 800, spp = 64, chunk = 16, bounces = 5, mode = 1, gpus = 1, ranks = 0;   // ogl_path_trace.h:45-46
     std::string pfm = "out.pfm", ppm = "out.ppm";
     float cam[12] = {0, -6, 1, 0, 0, 1, 0, 0, 0, 0, 0, 0};                          // ogl_path_trace.h:53-54
     bool robust = false, json = false, gpu_bvh = false;
@@ -165,6 +183,7 @@ int main(int argc, char** argv) {
         else if (a == "--bounces") bounces = std::atoi(next());
         else if (a == "--mode") mode = std::atoi(next());
         else if (a == "--gpus") gpus = std::atoi(next());
+        else if (a == "--ranks") ranks = std::atoi(next());
         else if (a == "--pfm") pfm = next();
         else if (a == "--ppm") ppm = next();
         else if (a == "--camera") { for (int k = 0; k < 6; k++) cam[k < 3 ? k : k + 1] = (float)std::atof(next()); }
@@ -176,16 +195,18 @@ int main(int argc, char** argv) {
         else if (a == "--gpu-bvh") gpu_bvh = true;
         else { usage(); return 2; }
     }
-    if (spp < 1 || chunk < 1 || gpus < 1) { usage(); return 2; }
+    if (ranks == 0) ranks = gpus;
+    if (spp < 1 || chunk < 1 || gpus < 1 || ranks < 1) { usage(); return 2; }
     if (events && (!resume.empty() || !checkpoint.empty())) {
         std::fprintf(stderr, "--events excludes --resume / --checkpoint\n");
         return 2;
     }
     int first = 1;                        // frame number of the first frame rendered
     std::vector<float> prior;
+    CkptKey saved = {};
     if (!resume.empty()) {
         std::string err;
-        if (!load_checkpoint(resume, W, H, first, prior, err)) { std::fprintf(stderr, "%s\n", err.c_str()); return 2; }
+        if (!load_checkpoint(resume, W, H, first, saved, prior, err)) { std::fprintf(stderr, "%s\n", err.c_str()); return 2; }
     }
 
     auto t0 = std::chrono::steady_clock::now();
@@ -207,12 +228,33 @@ int main(int argc, char** argv) {
     double t_scene = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
     std::printf("# of polygons: %d  # of materials: %d (+5 built-in)  # of spheres: %d  BVH nodes: %d  (%.3f s)\n",
                 cnt[0], cnt[4], cnt[2], cnt[3], t_scene);
+    const CkptKey key = {bounces, mode, cnt[0], cnt[3], {cam[0], cam[1], cam[2], cam[4], cam[5], cam[6]}};
+    if (!resume.empty() &&
+        (saved.bounces != key.bounces || saved.mode != key.mode || saved.tris != key.tris || saved.nodes != key.nodes ||
+         std::memcmp(saved.cam, key.cam, sizeof(key.cam)) != 0)) {
+        std::fprintf(stderr, "%s: checkpoint of a different render (bounces %d mode %d tris %d nodes %d camera "
+                             "%g %g %g %g %g %g); refusing to blend\n", resume.c_str(), saved.bounces, saved.mode,
+                     saved.tris, saved.nodes, saved.cam[0], saved.cam[1], saved.cam[2], saved.cam[3], saved.cam[4],
+                     saved.cam[5]);
+        return 2;
+    }
 
-    std::vector<pt_ctx*> ctx(gpus, nullptr);
-    for (int g = 0; g < gpus; g++) {
-        pt_config cfg = {W, H, bounces, mode, 0, 1, g, g, gpus};
+    const int nctx = ranks;
+    std::vector<pt_ctx*> ctx(nctx, nullptr);
+    for (int g = 0; g < nctx; g++) {
+        pt_config cfg = {W, H, bounces, mode, 0, 1, g % gpus, g, nctx};
         CHECK(pt_create(&cfg, &ctx[g]), ctx[g]);
-        CHECK(pt_upload_scene(ctx[g], tris.data(), cnt[0], nodes.data(), cnt[3], mats.data(), cnt[1], sph.data(), cnt[2]), ctx[g]);
+    }
+    pt_group* group = nullptr;
+    if (nctx > 1) {   // one RCCL communicator over the devices; the scene is validated once
+        int grc = pt_group_create(ctx.data(), nctx, &group);
+        if (!grc) grc = pt_group_upload_scene(group, tris.data(), cnt[0], nodes.data(), cnt[3], mats.data(), cnt[1],
+                                              sph.data(), cnt[2]);
+        if (grc) { std::fprintf(stderr, "pt_group: %s (%d)\n", pt_group_last_error(group), grc); return 1; }
+    }
+    for (int g = 0; g < nctx; g++) {
+        if (!group)
+            CHECK(pt_upload_scene(ctx[g], tris.data(), cnt[0], nodes.data(), cnt[3], mats.data(), cnt[1], sph.data(), cnt[2]), ctx[g]);
         CHECK(pt_set_camera(ctx[g], cam), ctx[g]);
         if (!prior.empty()) {             // this context's rows of the saved image
             int rows = 0, r0 = 0, rs = 1;
@@ -239,7 +281,7 @@ int main(int argc, char** argv) {
                 if (pt_viewer_should_close(view)) break;     // glfwWindowShouldClose (:160)
                 pt_viewer_frame_info fi;
                 pt_viewer_next(view, e.a, &fi);
-                for (int g = 0; g < gpus; g++) {
+                for (int g = 0; g < nctx; g++) {
                     CHECK(pt_set_display_mode(ctx[g], fi.display_mode), ctx[g]);
                     CHECK(pt_set_camera(ctx[g], fi.camera), ctx[g]);
                     CHECK(pt_render_async(ctx[g], fi.frame, 1, fi.accumulate), ctx[g]);
@@ -254,41 +296,47 @@ int main(int argc, char** argv) {
         for (int k = 0; k < spp; k += chunk) {
             const int n = std::min(chunk, spp - k), f0 = first + k;
             // frame 1 after a reset overwrites (accumulate = 0); a resumed run accumulates
-            for (int g = 0; g < gpus; g++) CHECK(pt_render_async(ctx[g], f0, n, f0 == 1 ? 0 : 1), ctx[g]);
+            for (int g = 0; g < nctx; g++) CHECK(pt_render_async(ctx[g], f0, n, f0 == 1 ? 0 : 1), ctx[g]);
         }
     }
-    for (int g = 0; g < gpus; g++) CHECK(pt_sync(ctx[g]), ctx[g]);
+    std::vector<float> img(4 * (size_t)W * H, 0.0f);
+    double gather_ms = 0.0;
+    if (group) {      // stream-ordered after every context's renders: the gather is the sync
+        int grc = pt_group_gather_rgba32f(group, img.data(), img.size() * 4, 0);
+        if (grc) { std::fprintf(stderr, "pt_group_gather_rgba32f: %s (%d)\n", pt_group_last_error(group), grc); return 1; }
+        pt_group_stats(group, &gather_ms, nullptr);
+    }
+    for (int g = 0; g < nctx; g++) CHECK(pt_sync(ctx[g]), ctx[g]);
     double secs = std::chrono::duration<double>(std::chrono::steady_clock::now() - t1).count();
     if (events) std::printf("replayed %s: %d frames, %d accumulation restarts\n", events, frames_run, resets);
 
-    std::vector<float> img(4 * (size_t)W * H, 0.0f);
     std::vector<unsigned char> rgba(4 * (size_t)W * H, 0);
-    for (int g = 0; g < gpus; g++) {
+    for (int g = 0; g < nctx; g++) {     // the ACES view is tonemapped on each context's device
         int rows = 0, r0 = 0, rs = 1;
         pt_rows(ctx[g], &rows, &r0, &rs);
-        std::vector<float> part(4 * (size_t)rows * W);
         std::vector<unsigned char> part8(4 * (size_t)rows * W);
-        CHECK(pt_read_rgba32f(ctx[g], part.data(), part.size() * 4), ctx[g]);
         CHECK(pt_read_rgba8_aces(ctx[g], part8.data(), part8.size()), ctx[g]);
-        for (int k = 0; k < rows; k++) {
-            int y = r0 + k * rs;
-            std::memcpy(&img[4 * (size_t)y * W], &part[4 * (size_t)k * W], 16 * (size_t)W);
-            std::memcpy(&rgba[4 * (size_t)y * W], &part8[4 * (size_t)k * W], 4 * (size_t)W);
-        }
-        pt_destroy(ctx[g]);
+        if (!group) CHECK(pt_read_rgba32f(ctx[g], img.data(), img.size() * 4), ctx[g]);
+        for (int k = 0; k < rows; k++)
+            std::memcpy(&rgba[4 * (size_t)(r0 + k * rs) * W], &part8[4 * (size_t)k * W], 4 * (size_t)W);
     }
-    std::printf("rendered %dx%d, %d spp, %d bounces on %d GPU(s): %.3f s, %.3f ms/frame\n", W, H, spp, bounces,
-                gpus, secs, secs * 1e3 / (spp > 0 ? spp : 1));
+    pt_group_destroy(group);
+    for (int g = 0; g < nctx; g++) pt_destroy(ctx[g]);
+    std::printf("rendered %dx%d, %d spp, %d bounces on %d GPU(s), %d context(s): %.3f s, %.3f ms/frame\n", W, H, spp,
+                bounces, gpus, nctx, secs, secs * 1e3 / (spp > 0 ? spp : 1));
+    if (group) std::printf("RCCL gather: %.3f ms\n", gather_ms);
     if (!checkpoint.empty()) {
-        if (!save_checkpoint(checkpoint, W, H, first + spp, img)) {
+        if (!save_checkpoint(checkpoint, W, H, first + spp, key, img)) {
             std::fprintf(stderr, "cannot write checkpoint %s\n", checkpoint.c_str());
             return 1;
         }
     }
     if (json)
         std::printf("{\"width\": %d, \"height\": %d, \"frames\": %d, \"first_frame\": %d, \"bounces\": %d, "
-                    "\"gpus\": %d, \"seconds\": %.6f, \"ms_per_frame\": %.4f, \"triangles\": %d, \"nodes\": %d}\n",
-                    W, H, spp, first, bounces, gpus, secs, secs * 1e3 / (spp > 0 ? spp : 1), cnt[0], cnt[3]);
+                    "\"gpus\": %d, \"contexts\": %d, \"seconds\": %.6f, \"ms_per_frame\": %.4f, \"triangles\": %d, "
+                    "\"nodes\": %d, \"gather_ms\": %.4f}\n",
+                    W, H, spp, first, bounces, gpus, nctx, secs, secs * 1e3 / (spp > 0 ? spp : 1), cnt[0], cnt[3],
+                    gather_ms);
 
     if (FILE* f = std::fopen(pfm.c_str(), "wb")) {       // PFM rows run bottom-to-top: no flip
         std::fprintf(f, "PF\n%d %d\n-1.0\n", W, H);

@@ -2224,6 +2224,56 @@ int pt_rows(const pt_ctx* c, int* rows_local, int* row0, int* row_stride) {
     return PT_OK;
 }
 
+int pt_get_config(const pt_ctx* c, pt_config* out) {
+    if (!c || !out) return PT_E_ARG;
+    *out = c->cfg;
+    return PT_OK;
+}
+
+// Scene replication for pt_group_upload_scene (pt_group.hip, not part of the public ABI):
+// gives `dst` a device scene of exactly `src`'s layout -- the same host-side facts and
+// buffers of the same sizes, contents undefined -- and returns both contexts' buffer pointers
+// and sizes, so the caller can fill dst's from src's (an RCCL broadcast across devices or a
+// device copy).  Both contexts must have the same width (tile facts are per image).
+int pt__scene_replicate_layout(pt_ctx* dst, const pt_ctx* src, void* dptr[6], const void* sptr[6],
+                               size_t bytes[6]) {
+    if (!dst || !src || !dptr || !sptr || !bytes) return PT_E_ARG;
+    if (!src->scene_ok) return fail(dst, PT_E_STATE, "source context has no scene");
+    HIPCHK(dst, hipSetDevice(dst->cfg.device));
+    HIPCHK(dst, hipStreamSynchronize(dst->stream));
+    drop_graph(dst);
+    free_scene(dst);
+    const size_t nd = 2 * (size_t)std::max(src->n_nodes, 1), nt = 8 * (size_t)std::max(src->n_slots / 2, 1);
+    const size_t nm = 3 * (size_t)std::max(src->n_mats, 1), ns = 2 * (size_t)std::max(src->n_spheres, 1);
+    const size_t nw = 16 * (size_t)src->walk_np, nk = src->d_walk_sk ? 18 * (size_t)src->walk_np : 0;
+    const size_t sz[6] = {nd, nt, nm, ns, nw, nk};
+    float4** mine[6] = {&dst->d_nodes, &dst->d_tris, &dst->d_mats, &dst->d_spheres, &dst->d_walk_lds, &dst->d_walk_sk};
+    const float4* theirs[6] = {src->d_nodes, src->d_tris, src->d_mats, src->d_spheres, src->d_walk_lds, src->d_walk_sk};
+    for (int i = 0; i < 6; i++) {
+        bytes[i] = sz[i] * sizeof(float4);
+        sptr[i] = theirs[i];
+        if (sz[i]) HIPCHK(dst, hipMalloc(mine[i], bytes[i]));
+        dptr[i] = *mine[i];
+    }
+    dst->n_nodes = src->n_nodes;
+    dst->n_spheres = src->n_spheres;
+    dst->n_mats = src->n_mats;
+    dst->n_slots = src->n_slots;
+    dst->n_top = src->n_top;
+    dst->scene_fast = src->scene_fast;
+    dst->walk_nested = src->walk_nested;
+    std::memcpy(dst->cons_m, src->cons_m, sizeof(dst->cons_m));
+    dst->walk_np = src->walk_np;
+    dst->lds_bytes = src->lds_bytes;
+    dst->lds_bytes_sk = src->lds_bytes_sk;
+    std::memcpy(dst->root_box, src->root_box, sizeof(dst->root_box));
+    dst->root_child = src->root_child;
+    dst->order_sorted = false;
+    dst->order_skip = 0;
+    dst->scene_ok = true;
+    return PT_OK;
+}
+
 int pt_read_rgba32f(pt_ctx* c, float* dst, size_t bytes) {
     if (!c || !dst) return PT_E_ARG;
     size_t need = (size_t)c->rows_local * c->cfg.width * sizeof(float4);

@@ -33,3 +33,32 @@ def gather_image(local_rows, height, world, group=None):
     out = torch.empty((world * rmax, W, C), dtype=local_rows.dtype, device=local_rows.device)
     dist.all_gather_into_tensor(out, local_rows.contiguous(), group=group)
     return interleave(out.view(world, rmax, W, C), height)
+
+
+_SCENE_KEYS = (("tris", 16), ("nodes", 12), ("mats", 16), ("spheres", 8))
+
+
+def broadcast_scene(sb, device="cpu", src=0, group=None):
+    """The scene of setupBuffers() from rank `src` to every rank (the OBJ is parsed and the
+    BVH built once, not per rank).  sb: the SceneBuffers on `src`, ignored
+    elsewhere.  Returns the scene dict (tris, nodes, mats, spheres, cam, n_loaded_mats) on every
+    rank; tensors travel on `device` ("cuda" for RCCL, "cpu" for gloo)."""
+    import numpy as np
+    rank = dist.get_rank(group)
+    counts = torch.zeros(5, dtype=torch.int64, device=device)
+    if rank == src:
+        counts[:] = torch.tensor([len(np.asarray(sb[k]).reshape(-1, c)) for k, c in _SCENE_KEYS] +
+                                 [int(sb["n_loaded_mats"])], dtype=torch.int64)
+    dist.broadcast(counts, src, group=group)
+    n = [int(v) for v in counts.cpu()]
+    out = {}
+    for (k, c), m in zip(_SCENE_KEYS + (("cam", 12),), n[:4] + [1]):
+        t = torch.empty((m, c), dtype=torch.float32, device=device)
+        if rank == src:
+            t.copy_(torch.from_numpy(np.ascontiguousarray(sb[k], np.float32).reshape(m, c)))
+        if m:
+            dist.broadcast(t, src, group=group)
+        out[k] = t.cpu().numpy()
+    out["cam"] = out["cam"].reshape(12)
+    out["n_loaded_mats"] = n[4]
+    return out

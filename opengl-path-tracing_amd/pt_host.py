@@ -32,7 +32,8 @@ PT_FLAG_NO_AA, PT_FLAG_NO_SKY, PT_FLAG_NO_SPHERES, PT_FLAG_NO_TRIANGLES, PT_FLAG
 PT_FLAG_MOLLER_TRUMBORE = 32   # opt-in fast triangle test (not the reference image; see pt_api.h)
 DEFAULT_CAMERA = np.array([0, -6, 1, 0, 0, 1, 0, 0, 0, 0, 0, 0], np.float32)  # ogl_path_trace.h:53-54
 
-_ERR = {-1: "PT_E_ARG", -2: "PT_E_IO", -3: "PT_E_PARSE", -4: "PT_E_SCENE", -5: "PT_E_HIP", -6: "PT_E_STATE"}
+_ERR = {-1: "PT_E_ARG", -2: "PT_E_IO", -3: "PT_E_PARSE", -4: "PT_E_SCENE", -5: "PT_E_HIP", -6: "PT_E_STATE",
+        -7: "PT_E_RCCL"}
 
 
 class PTError(RuntimeError):
@@ -113,6 +114,14 @@ def lib():
             "pt_progressive_reset": (ip, [vp, ip]),
             "pt_progressive_run": (ip, [vp, ip]),
             "pt_set_display_mode": (ip, [vp, ip]),
+            "pt_get_config": (ip, [vp, C.POINTER(_Config)]),
+            "pt_group_create": (ip, [C.POINTER(vp), ip, C.POINTER(vp)]),
+            "pt_group_destroy": (None, [vp]),
+            "pt_group_last_error": (C.c_char_p, [vp]),
+            "pt_group_upload_scene": (ip, [vp, _F, ip, _F, ip, _F, ip, _F, ip]),
+            "pt_group_gather_rgba32f": (ip, [vp, vp, C.c_size_t, ip]),
+            "pt_group_stats": (ip, [vp, C.POINTER(C.c_double), C.POINTER(C.c_size_t)]),
+            "pt_gather_rgba32f": (ip, [C.POINTER(vp), ip, vp, C.c_size_t, ip]),
             "pt_viewer_create": (ip, [vp, ip, C.POINTER(vp)]),
             "pt_viewer_destroy": (None, [vp]),
             "pt_viewer_set_params": (ip, [vp, fp, fp, ip]),
@@ -134,7 +143,7 @@ def header_symbols():
     """Function names declared in include/*.h (for the ABI export test)."""
     import re
     names = []
-    for h in ("pt_api.h", "pt_scene.h", "pt_viewer.h"):
+    for h in ("pt_api.h", "pt_scene.h", "pt_viewer.h", "pt_group.h"):
         txt = open(os.path.join(INCLUDE_DIR, h)).read()
         txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
         names += re.findall(r"\b(pt_[a-z0-9_]+)\s*\(", txt)
@@ -476,6 +485,76 @@ class Viewer:
         if rc:
             raise PTError(rc, lib().pt_last_error(pt.h).decode())
         return self._info(fi)
+
+
+class Group:
+    """pt_group.h: one process, several row-split contexts of one image -- the scene
+    validated once and broadcast over RCCL, the frame gathered over RCCL and interleaved on the
+    first context's device."""
+
+    def __init__(self, tracers):
+        self.tracers = list(tracers)
+        arr = (C.c_void_p * len(self.tracers))(*[t.h for t in self.tracers])
+        h = C.c_void_p()
+        rc = lib().pt_group_create(arr, len(self.tracers), C.byref(h))
+        self.h = h
+        if rc:
+            msg = lib().pt_group_last_error(h).decode() if h.value else ""
+            self.close()
+            raise PTError(rc, msg)
+        t0 = self.tracers[0]
+        self.W, self.H = t0.width, t0.height
+
+    def _check(self, rc):
+        if rc:
+            raise PTError(rc, lib().pt_group_last_error(self.h).decode())
+
+    def upload(self, sb):
+        t, n, m, s = (_f32(sb["tris"], 16), _f32(sb["nodes"], 12), _f32(sb["mats"], 16), _f32(sb["spheres"], 8))
+        flat = lambda a, c: a.reshape(-1) if len(a) else np.zeros(c, np.float32)
+        self._check(lib().pt_group_upload_scene(self.h, flat(t, 16), len(t), flat(n, 12), len(n), flat(m, 16), len(m),
+                                                flat(s, 8), len(s)))
+        if "cam" in sb:
+            for tr in self.tracers:
+                tr.set_camera(sb["cam"])
+
+    def gather(self, device_ptr=None):
+        """The full (H, W, 4) frame: to host (numpy), or into device memory at device_ptr on the
+        first context's device (returns None)."""
+        nbytes = self.W * self.H * 16
+        if device_ptr is not None:
+            self._check(lib().pt_group_gather_rgba32f(self.h, C.c_void_p(device_ptr), nbytes, 1))
+            return None
+        out = np.zeros((self.H, self.W, 4), np.float32)
+        self._check(lib().pt_group_gather_rgba32f(self.h, out.ctypes.data, nbytes, 0))
+        return out
+
+    def stats(self):
+        ms, b = C.c_double(), C.c_size_t()
+        self._check(lib().pt_group_stats(self.h, C.byref(ms), C.byref(b)))
+        return ms.value, b.value
+
+    def close(self):
+        if getattr(self, "h", None) is not None and self.h.value:
+            lib().pt_group_destroy(self.h)
+        self.h = C.c_void_p()
+
+
+def gather_rgba32f(tracers, device_ptr=None):
+    """pt_gather_rgba32f: one-shot group + gather."""
+    t0 = tracers[0]
+    arr = (C.c_void_p * len(tracers))(*[t.h for t in tracers])
+    nbytes = t0.width * t0.height * 16
+    if device_ptr is not None:
+        rc = lib().pt_gather_rgba32f(arr, len(tracers), C.c_void_p(device_ptr), nbytes, 1)
+        if rc:
+            raise PTError(rc, "pt_gather_rgba32f")
+        return None
+    out = np.zeros((t0.height, t0.width, 4), np.float32)
+    rc = lib().pt_gather_rgba32f(arr, len(tracers), out.ctypes.data, nbytes, 0)
+    if rc:
+        raise PTError(rc, "pt_gather_rgba32f")
+    return out
 
 
 def assemble_rows(parts, height):

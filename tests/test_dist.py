@@ -28,6 +28,12 @@ def _worker(rank, world, port, sc, out):
     import torch.distributed as dist
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
+    # rank 0 holds the scene; the others receive it (bench.py's broadcast)
+    got = pt_dist.broadcast_scene(sc if rank == 0 else None)
+    for k in ("tris", "nodes", "mats", "spheres", "cam"):
+        assert np.array_equal(np.asarray(got[k]).view(np.uint32), np.asarray(sc[k], np.float32).view(np.uint32)), k
+    assert got["n_loaded_mats"] == sc["n_loaded_mats"]
+    sc = got
     rows = np.arange(rank, H, world)
     ys, xs = np.meshgrid(rows, np.arange(W), indexing="ij")
     px = O.render_pixels(sc, W, H, xs.reshape(-1), ys.reshape(-1), max_bounce=MB, n_frames=SPP, threads=2)
@@ -57,6 +63,7 @@ def _run(world, sc):
 
 def test_gloo_two_rank_gather_is_bit_identical(cornell_scene):
     sc = {k: np.asarray(v) for k, v in cornell_scene.items()}
+    sc["n_loaded_mats"] = int(cornell_scene["n_loaded_mats"])
     full = O.render(sc, W, H, max_bounce=MB, n_frames=SPP)
     img = _run(2, sc)
     assert np.array_equal(img.view(np.uint32), full.view(np.uint32))

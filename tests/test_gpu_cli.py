@@ -64,7 +64,10 @@ def test_cli_checkpoint_resume_is_one_run(tmp_path, gpus):
                        capture_output=True, text=True, timeout=120)
     assert a.returncode == 0, a.stderr
     with open(ck, "rb") as f:
-        assert f.readline().split() == [b"PTCK1", str(W).encode(), str(Hh).encode(), b"5"]
+        head = f.readline().split()
+    # PTCK2 W H next_frame bounces mode tris nodes camera(6)
+    assert head[:8] == [b"PTCK2", str(W).encode(), str(Hh).encode(), b"5", b"8", b"1", b"36", b"35"]
+    assert [float(v) for v in head[8:]] == [0.0, -6.0, 1.0, 0.0, 1.0, 0.0]
     b = subprocess.run(common + ["--spp", "3", "--resume", ck, "--pfm", str(tmp_path / "b.pfm"), "--json"],
                        capture_output=True, text=True, timeout=120)
     assert b.returncode == 0, b.stderr
@@ -76,12 +79,55 @@ def test_cli_checkpoint_resume_is_one_run(tmp_path, gpus):
     assert np.array_equal(got.view(np.uint32), np.ascontiguousarray(want[..., :3]).view(np.uint32))
 
 
+CK_HEAD = b"PTCK2 8 8 3 5 1 36 35 0 -6 1 0 1 0\n"
+
+
 def test_cli_rejects_bad_checkpoint(tmp_path, cornell_paths):
     bad = tmp_path / "bad.ptck"
-    bad.write_bytes(b"PTCK1 8 8 3\n" + b"\0" * 16)
+    bad.write_bytes(CK_HEAD + b"\0" * 16)
     out = subprocess.run([EXE, *cornell_paths, "--width", "8", "--height", "8", "--resume", str(bad)],
                          capture_output=True, text=True, timeout=60)
     assert out.returncode == 2 and "truncated" in out.stderr
     out = subprocess.run([EXE, *cornell_paths, "--width", "9", "--height", "8", "--resume", str(bad)],
                          capture_output=True, text=True, timeout=60)
     assert out.returncode == 2 and "checkpoint is 8x8" in out.stderr
+
+
+def test_cli_refuses_checkpoint_of_another_render(tmp_path, cornell_paths):
+    """--resume checks bounces, display mode, the scene's triangle / node counts and the
+    camera recorded in the PTCK2 header: a mismatch is refused, not blended.
+    The check runs before any device work, so this runs on CPU."""
+    ck = tmp_path / "ok.ptck"
+    ck.write_bytes(CK_HEAD + b"\0" * (8 * 8 * 16))
+    for extra in (["--bounces", "4"], ["--mode", "2"], ["--camera", "0", "-5", "1", "0", "1", "0"]):
+        out = subprocess.run([EXE, *cornell_paths, "--width", "8", "--height", "8", "--resume", str(ck), *extra],
+                             capture_output=True, text=True, timeout=60)
+        assert out.returncode == 2 and "refusing to blend" in out.stderr, (extra, out.stderr)
+    old = tmp_path / "old.ptck"
+    old.write_bytes(b"PTCK1 8 8 3\n" + b"\0" * (8 * 8 * 16))
+    out = subprocess.run([EXE, *cornell_paths, "--width", "8", "--height", "8", "--resume", str(old)],
+                         capture_output=True, text=True, timeout=60)
+    assert out.returncode == 2 and "not a PTCK2 checkpoint" in out.stderr
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("ranks,chunk", [(4, 2), (3, 5)])
+def test_cli_ranks_gather_over_rccl(tmp_path, ranks, chunk):
+    """--ranks R: R row-split contexts on this one GPU, the scene validated once and broadcast,
+    the frame gathered by pt_group (RCCL, a 1-rank communicator here) -- the same PFM bits as
+    one context and as the oracle, and the same ACES view."""
+    obj, mtl = pt_scenes.write_scene("cornell", str(tmp_path))
+    W, Hh, spp = 72, 50, 5
+    outs = {}
+    for r in (1, ranks):
+        pfm, ppm = str(tmp_path / ("o%d.pfm" % r)), str(tmp_path / ("o%d.ppm" % r))
+        out = subprocess.run([EXE, obj, mtl, "--width", str(W), "--height", str(Hh), "--spp", str(spp), "--chunk",
+                              str(chunk), "--bounces", "8", "--ranks", str(r), "--pfm", pfm, "--ppm", ppm, "--json"],
+                             capture_output=True, text=True, timeout=120)
+        assert out.returncode == 0, out.stderr
+        outs[r] = (read_pfm(pfm), read_ppm(ppm))
+    assert "RCCL gather" in out.stdout
+    assert np.array_equal(outs[1][0].view(np.uint32), outs[ranks][0].view(np.uint32))
+    assert np.array_equal(outs[1][1], outs[ranks][1])
+    want = O.render(H.setupBuffers(obj, mtl), W, Hh, max_bounce=8, n_frames=spp)
+    assert np.array_equal(outs[ranks][0].view(np.uint32), np.ascontiguousarray(want[..., :3]).view(np.uint32))

@@ -1,0 +1,85 @@
+"""pt_group.h on one GPU: G row-split contexts of one image with the scene validated once and
+broadcast, and the frame gathered over RCCL (a 1-rank communicator when every context shares
+the device) -- bit-identical to one context's render and to the oracle (SURVEY.md §8(e);
+replaces the single context's dispatch + blit, ogl_path_trace.h:183-192).  8-GPU runs are the
+driver's; the gather code path (pack, ncclGather, interleave kernel) is the same."""
+import numpy as np
+import pytest
+
+import oracle_lib as O
+import pt_host as H
+from test_gpu_parity import assert_bitwise
+
+pytestmark = pytest.mark.gpu
+
+
+def split_render(sc, W, Hh, world, frames, max_bounce=8, order=None):
+    order = list(range(world)) if order is None else order
+    trs = [H.PathTracer(W, Hh, max_bounce=max_bounce, rank=r, world=world) for r in order]
+    g = H.Group(trs)
+    g.upload(sc)
+    for t in trs:
+        t.render_async(1, frames, 0)
+    return g, trs
+
+
+@pytest.mark.parametrize("world", [1, 3, 8])
+def test_group_gather_equals_one_context(cornell_scene, ship_scene, world):
+    for sc in (cornell_scene, ship_scene):
+        W, Hh = 80, 53
+        want = O.render(sc, W, Hh, max_bounce=8, n_frames=4)
+        g, trs = split_render(sc, W, Hh, world, 4, order=list(range(world))[::-1])
+        got = g.gather()
+        ms, nbytes = g.stats()
+        g.close()
+        for t in trs:
+            t.close()
+        assert_bitwise(got, want, "world %d" % world)
+        assert nbytes == world * ((Hh + world - 1) // world) * W * 16 and ms >= 0.0
+
+
+def test_group_gather_into_device_memory(cornell_scene):
+    import torch
+    W, Hh, world = 96, 40, 4
+    want = O.render(cornell_scene, W, Hh, max_bounce=6, n_frames=3)
+    g, trs = split_render(cornell_scene, W, Hh, world, 3, max_bounce=6)
+    out = torch.full((Hh, W, 4), float("nan"), dtype=torch.float32, device="cuda:0")
+    torch.cuda.synchronize()
+    g.gather(device_ptr=out.data_ptr())
+    got = out.cpu().numpy()
+    one = H.gather_rgba32f(trs)                    # one-shot form, host destination
+    g.close()
+    for t in trs:
+        t.close()
+    assert_bitwise(got, want, "device destination")
+    assert_bitwise(one, want, "pt_gather_rgba32f")
+
+
+def test_group_broadcast_global_memory_scene(tmp_path):
+    """A scene too large for LDS (the global-memory walk with its breadth-first top nodes):
+    the broadcast copies every device buffer and the walk facts; 1080p split 8 ways."""
+    import pt_scenes
+    sc = H.setupBuffers(*pt_scenes.write_scene("bunny", str(tmp_path), target_tris=5000))
+    W, Hh = 1920, 1080
+    g, trs = split_render(sc, W, Hh, 8, 2)
+    got = g.gather()
+    g.close()
+    for t in trs:
+        t.close()
+    rng = np.random.default_rng(9)
+    xs = np.concatenate([rng.integers(0, W, 3000), np.arange(W)])
+    ys = np.concatenate([rng.integers(0, Hh, 3000), np.full(W, Hh - 1)])
+    want = O.render_pixels(sc, W, Hh, xs, ys, max_bounce=8, n_frames=2)
+    assert_bitwise(got[ys, xs], want, "global scene, 8-way split")
+
+
+def test_group_rejects_inconsistent_contexts(cornell_scene):
+    a = H.PathTracer(32, 16, rank=0, world=2)
+    b = H.PathTracer(40, 16, rank=1, world=2)
+    c = H.PathTracer(32, 16, rank=0, world=2)
+    for trs in ([a, b], [a, c], [a]):
+        with pytest.raises(H.PTError) as e:
+            H.Group(trs)
+        assert e.value.code == -1
+    for t in (a, b, c):
+        t.close()
