@@ -73,7 +73,8 @@ int pt_viewer_should_close(const pt_viewer* v);
  * (glfwGetTime() seconds).  Fills *out with the dispatch parameters. */
 int pt_viewer_next(pt_viewer* v, double now, pt_viewer_frame_info* out);
 /* pt_viewer_next, then on ctx: display mode, camera, and one dispatch
- * pt_render(frame, 1, accumulate).  out may be NULL. */
+ * pt_render_async(frame, 1, accumulate) -- enqueued, like glDispatchCompute; a readback or
+ * pt_sync waits for it.  out may be NULL. */
 int pt_viewer_frame(pt_viewer* v, pt_ctx* ctx, double now, pt_viewer_frame_info* out);
 
 #ifdef __cplusplus

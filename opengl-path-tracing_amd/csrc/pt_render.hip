@@ -522,6 +522,11 @@ __device__ __forceinline__ void leaf_pair_tests(const SceneView& S, bool at, int
 // =====================================================================================
 enum : int { ST_DONE = 0, ST_TRAV = 1, ST_LEAF = 2, ST_SHADE = 3 };
 constexpr unsigned kPullBatch = 32;
+// frame-split work queue: kShards heads, kShardStride unsigned apart (own 128-B lines)
+#ifndef PT_SHARDS
+#define PT_SHARDS 8
+#endif
+constexpr int kShards = PT_SHARDS, kShardStride = 32;
 #ifndef PT_WALK_UNROLL
 #define PT_WALK_UNROLL 4
 #endif
@@ -654,8 +659,20 @@ __device__ __forceinline__ void trav_walk(const SceneView& S, f3 o, f3 d, f3 rd,
 __device__ unsigned long long g_phase_clk[8];
 #endif
 
+#ifdef PT_WAVE_TRACE
+// experiment builds only (-DPT_WAVE_TRACE): per wave of the last render launch, the wall clock
+// (s_memrealtime, 100 MHz) at kernel entry, after the LDS staging and at exit, and the work
+// items it took; read back by pt_debug_wave_trace
+constexpr int kWaveTraceMax = 16384;
+__device__ unsigned long long g_wave_trace[kWaveTraceMax * 4];
+#endif
+
 template <bool COUNT, bool LDS, int MINW, bool MULTI, bool SPLIT, bool PADN = false, int NT = 256>
 __global__ __launch_bounds__(NT, MINW) void k_render_sm(KParams p) {
+#ifdef PT_WAVE_TRACE
+    const unsigned long long wt_entry = __builtin_amdgcn_s_memrealtime();
+    unsigned wt_items = 0;
+#endif
     resolve_frames(p);
     extern __shared__ float4 lds[];
     SceneView S;
@@ -713,11 +730,15 @@ __global__ __launch_bounds__(NT, MINW) void k_render_sm(KParams p) {
     const int tiles_x = (p.W + 7) >> 3;
     const unsigned n_groups = SPLIT ? (unsigned)((p.n_frames + p.group - 1) / p.group) : 1u;
     const unsigned total_ids = (unsigned)tiles_x * (unsigned)((p.rows_local + 7) >> 3) * n_groups * 64u;
+    const unsigned n_items = total_ids >> 6;
     const int n_nodes = p.sc.n_nodes;
     const bool use_tris = !(p.flags & PT_FLAG_NO_TRIANGLES) && n_nodes > 0;
     // walk start for a ray inside the root box: its first child (the counting build walks
     // from the root, so the counts stay the reference's)
     const int root_skip = (COUNT || p.root_child < 0) ? -1 : p.root_child << (LDS ? 4 : 0);
+#ifdef PT_WAVE_TRACE
+    const unsigned long long wt_staged = __builtin_amdgcn_s_memrealtime();
+#endif
 
     Cnt c = {0, 0, 0, 0, 0};
     int st = ST_SHADE;
@@ -727,6 +748,7 @@ __global__ __launch_bounds__(NT, MINW) void k_render_sm(KParams p) {
     int aidx = 0;             // rows_local * W < 2^31 (checked at pt_create)
     int k = 0, kend = 0, r = 0, bounce = 0;   // frames k..kend-1 of this work item
     unsigned qnext = 0, qend = 0;             // wave's reserved queue ids (frame-split mode)
+    unsigned qshard = blockIdx.x % kShards, qtried = 0;   // its shard; shards found dry in a row
     unsigned tile_id = 0, pcost = 0;    // adaptive queue order: this pixel's tile + segments
     float4 acc = make_float4(0, 0, 0, 0);
     f3 psum = mk(0, 0, 0), o = mk(0, 0, 0), d = mk(0, 0, 1), inc = mk(0, 0, 0), col = mk(1, 1, 1);
@@ -859,8 +881,13 @@ __global__ __launch_bounds__(NT, MINW) void k_render_sm(KParams p) {
                 lx = -1;
             }
             // wave-aggregated pull from the work queue.  Frame-split items are short, so
-            // there a wave reserves ids in batches of kPullBatch (one queue atomic per
-            // batch instead of per pull; the counter is one address for the whole chip).
+            // there a wave reserves ids in batches of pull_batch (one queue atomic per batch
+            // instead of per pull), and the queue is sharded (kShards heads, shard s owns
+            // items s, s + kShards, ...: each shard keeps the expensive-first tile order): one
+            // device-scope head saturates near 88 dequeues per microsecond, which bounded the
+            // one-frame launches.  A wave starts on shard blockIdx mod kShards (its XCD) and
+            // moves on when that shard runs dry; it is done once it has found kShards shards
+            // dry in a row.  Register mode keeps one head (long items, few pulls).
             bool want = st == ST_SHADE && lx < 0;
             unsigned long long m = __ballot(want);
             if (m) {
@@ -868,26 +895,43 @@ __global__ __launch_bounds__(NT, MINW) void k_render_sm(KParams p) {
                 const unsigned rank = (unsigned)rank_in(m);
                 const int leader = __ffsll((long long)m) - 1;
                 unsigned id;
+                bool valid = true;
+                const unsigned sh = qshard;
                 if (SPLIT && qend - qnext >= need) {
                     id = qnext + rank;
                     qnext += need;
-                } else {
-                    const unsigned avail = SPLIT ? qend - qnext : 0u;
-                    const unsigned take = SPLIT ? max(need - avail, (unsigned)p.pull_batch) : need;
+                    qtried = 0;
+                } else if (SPLIT) {
+                    const unsigned shard_ids = ((n_items + (kShards - 1) - sh) / kShards) * 64u;
+                    const unsigned avail = qend - qnext;
+                    const unsigned take = max(need - avail, (unsigned)p.pull_batch);
                     unsigned base = 0;
-                    if (want && rank == 0u) base = atomicAdd(p.work_counter, take);   // the leader
+                    if (want && rank == 0u) base = atomicAdd(p.work_counter + kShardStride * sh, take);   // the leader
                     base = (unsigned)__builtin_amdgcn_readlane((int)base, leader);
                     id = rank < avail ? qnext + rank : base + (rank - avail);
-                    if (SPLIT) {
-                        qnext = base + (need - avail);
-                        qend = base + take;
+                    valid = id < shard_ids;
+                    qnext = base + (need - avail);
+                    qend = base + take < shard_ids ? base + take : shard_ids;
+                    // shards found dry with lanes left unserved, in a row
+                    qtried = qnext <= shard_ids ? 0u : qtried + 1u;
+                    if (qnext >= qend) {       // this shard ran dry: the next one
+                        qnext = qend = 0u;
+                        qshard = sh + 1u == (unsigned)kShards ? 0u : sh + 1u;
                     }
+                } else {
+                    unsigned base = 0;
+                    if (want && rank == 0u) base = atomicAdd(p.work_counter, need);   // the leader
+                    base = (unsigned)__builtin_amdgcn_readlane((int)base, leader);
+                    id = base + rank;
+                    valid = id < total_ids;
                 }
                 if (want) {
-                    if (id >= total_ids) {
-                        st = ST_DONE;
+                    if (!valid) {
+                        // register mode: the queue is empty; split mode: empty once every
+                        // shard has been found dry, else retry on the next shard
+                        if (!SPLIT || qtried >= (unsigned)kShards) st = ST_DONE;
                     } else {
-                        const unsigned item = id >> 6, w = id & 63u;
+                        const unsigned item = SPLIT ? (id >> 6) * (unsigned)kShards + sh : id >> 6, w = id & 63u;
                         // item -> (tile, frame group): by the host's exact magic reciprocal
                         // (kernel argument) when it is valid for every item
                         unsigned tile = item;
@@ -908,6 +952,9 @@ __global__ __launch_bounds__(NT, MINW) void k_render_sm(KParams p) {
                         int cy = p.row0 + crow * p.row_stride;
                         if ((cx < p.W) & (crow < p.rows_local) & (cx < p.x_limit) & (cy < p.y_limit)) {
                             lx = cx;
+#ifdef PT_WAVE_TRACE
+                            wt_items++;
+#endif
                             y = cy;
                             aidx = crow * p.W + cx;
                             // cost sample: 4 pixels per 8x8 tile report (one 64-B memory-side
@@ -1072,6 +1119,20 @@ __global__ __launch_bounds__(NT, MINW) void k_render_sm(KParams p) {
         if (lane == 0) { atomicAdd(&g_phase_clk[6], tw); atomicAdd(&g_phase_clk[7], tl); }
     }
 #endif
+#ifdef PT_WAVE_TRACE
+    {
+        const unsigned long long wt_end = __builtin_amdgcn_s_memrealtime();
+        unsigned items = wt_items;
+        for (int off = 32; off > 0; off >>= 1) items += __shfl_xor(items, off, 64);
+        const int wid = blockIdx.x * (NT / 64) + (int)(threadIdx.x >> 6);
+        if ((threadIdx.x & 63) == 0 && wid < kWaveTraceMax) {
+            g_wave_trace[4 * wid] = wt_entry;
+            g_wave_trace[4 * wid + 1] = wt_staged;
+            g_wave_trace[4 * wid + 2] = wt_end;
+            g_wave_trace[4 * wid + 3] = items;
+        }
+    }
+#endif
     flush_counters<COUNT>(p, c);
 }
 
@@ -1170,6 +1231,12 @@ constexpr size_t kLdsSceneSmall = 48 * 1024;  // staged by 256-thread workgroups
 // global-memory scenes: the first kTopNodes device nodes (breadth-first from the root) are
 // staged in LDS, 24 KiB per workgroup (6 workgroups per CU stay resident)
 constexpr int kTopNodes = 768;
+// overlapped short launches: render slots (tuning key 9).  A slot's scratch is reused only
+// after the accumulate pass that read it, and that pass gets CUs only as render blocks retire,
+// so with 2 slots render f+1 waited for the end of render f (measured 0.61 ms per 1080p frame);
+// with 3 it waits only for render f-1.
+constexpr int kMaxSlots = 4, kAutoSlots = 3;
+constexpr size_t kQueueSet = (size_t)kShards * kShardStride;   // unsigned per set of queue heads
 
 struct pt_ctx {
     pt_config cfg{};
@@ -1221,6 +1288,21 @@ struct pt_ctx {
     int n_cu = 0;
     float* d_rgb = nullptr;        // per-(frame, pixel) colours of the frame-split mode
     size_t rgb_bytes = 0;
+    // overlapped short launches (enqueue_render): the render kernels of consecutive short
+    // renders rotate over `n_slots` streams with their own colour scratch and queue counter,
+    // so frame f+1 renders while frame f's launch drains; k_accum_frames stays on `stream`
+    // (created with the highest priority, so its small grid is dispatched as soon as render
+    // blocks retire) in frame order
+    hipStream_t rstream[kMaxSlots] = {};
+    float* slot_rgb[kMaxSlots] = {};
+    size_t slot_rgb_bytes[kMaxSlots] = {};
+    hipEvent_t ev_rdone[kMaxSlots] = {}, ev_adone[kMaxSlots] = {};
+    // main-stream fence an overlapped render waits for: recorded after every tile-order sort
+    // and graph replay (the writers of tile_perm, which the render reads)
+    hipEvent_t ev_fence = nullptr;
+    bool adone_rec[kMaxSlots] = {}, fence_rec = false;
+    int slot = 0;
+    int overlap_slots = kAutoSlots;   // tuning key 9 (1 = one stream, no overlap)
     // frame-split scratch budget: a render needing more is issued as back-to-back launches
     // (tuning key 8; default min(32 GiB, a quarter of the device memory))
     size_t scratch_budget = 0;
@@ -1334,12 +1416,19 @@ int pt_create(const pt_config* cfg, pt_ctx** out) {
     c->rows_local = cfg->height > rank ? (cfg->height - rank + world - 1) / world : 0;
     if ((long long)c->rows_local * cfg->width >= (1LL << 31)) return fail(c, PT_E_ARG, "framebuffer exceeds 2^31 pixels");
     size_t px = (size_t)c->rows_local * cfg->width;
-    HIPCHK(c, hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+    {
+        int lo = 0, hi = 0;   // hi = the greatest priority (numerically least)
+        HIPCHK(c, hipDeviceGetStreamPriorityRange(&lo, &hi));
+        HIPCHK(c, hipStreamCreateWithPriority(&c->stream, hipStreamNonBlocking, hi));
+    }
+    HIPCHK(c, hipEventCreateWithFlags(&c->ev_fence, hipEventDisableTiming));
     HIPCHK(c, hipMalloc(&c->accum, std::max<size_t>(px, 1) * sizeof(float4)));
     HIPCHK(c, hipMemset(c->accum, 0, std::max<size_t>(px, 1) * sizeof(float4)));
     HIPCHK(c, hipMalloc(&c->rgba8, std::max<size_t>(px, 1) * sizeof(uchar4)));
     HIPCHK(c, hipMalloc(&c->d_counters, 16 * sizeof(unsigned long long)));
-    HIPCHK(c, hipMalloc(&c->d_work, 64));
+    // work-queue heads: one set of kShards heads (kShardStride apart) for the main stream and
+    // one per overlap slot
+    HIPCHK(c, hipMalloc(&c->d_work, kQueueSet * sizeof(unsigned) * (1 + kMaxSlots)));
     int n_cu = 0;
     HIPCHK(c, hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, cfg->device));
     c->persist_blocks = (unsigned)std::max(1, n_cu) * 8u;   // 8 x 256 threads = 32 waves per CU
@@ -1376,6 +1465,14 @@ void pt_destroy(pt_ctx* c) {
     (void)hipFree(c->d_tile_perm);
     (void)hipFree(c->d_tile_cost);
     (void)hipFree(c->d_rgb);
+    for (int i = 0; i < kMaxSlots; i++) {
+        (void)hipFree(c->slot_rgb[i]);
+        if (c->rstream[i]) (void)hipStreamSynchronize(c->rstream[i]);
+        if (c->rstream[i]) (void)hipStreamDestroy(c->rstream[i]);
+        if (c->ev_rdone[i]) (void)hipEventDestroy(c->ev_rdone[i]);
+        if (c->ev_adone[i]) (void)hipEventDestroy(c->ev_adone[i]);
+    }
+    if (c->ev_fence) (void)hipEventDestroy(c->ev_fence);
     for (auto& pr : c->ev_pending) { c->ev_free.push_back(pr.first); c->ev_free.push_back(pr.second); }
     for (hipEvent_t e : c->ev_free) (void)hipEventDestroy(e);
     if (c->stream) (void)hipStreamDestroy(c->stream);
@@ -1722,6 +1819,15 @@ int pt_set_tuning(pt_ctx* c, int key, int value) {
         drop_graph(c);
         return PT_OK;
     }
+    if (key == 9) {
+        if (value < 0 || value > kMaxSlots)
+            return fail(c, PT_E_ARG, "overlap slots must be 1..4 (1 = off, 0 = automatic)");
+        HIPCHK(c, hipSetDevice(c->cfg.device));
+        HIPCHK(c, hipStreamSynchronize(c->stream));
+        c->overlap_slots = value ? value : kAutoSlots;
+        c->slot = 0;
+        return PT_OK;
+    }
     if (key == 15) {
         if (value != 0 && value != 1) return fail(c, PT_E_ARG, "culling walk: 0 = automatic, 1 = off");
         c->cons_off = value;
@@ -1834,6 +1940,27 @@ static int ensure_rgb(pt_ctx* c, int n_frames) {
     c->rgb_bytes = 0;
     HIPCHK(c, hipMalloc(&c->d_rgb, need));
     c->rgb_bytes = need;
+    return PT_OK;
+}
+
+// Scratch, stream and events of overlap slot `sl` (enqueue_render), created on first use.  The
+// slot's buffer may still be read by the accumulate pass of the last launch that used it, so
+// a reallocation first drains the main stream and the slot's render stream.
+static int ensure_slot(pt_ctx* c, int sl, int n_frames) {
+    if (!c->rstream[sl]) {
+        HIPCHK(c, hipStreamCreateWithFlags(&c->rstream[sl], hipStreamNonBlocking));
+        HIPCHK(c, hipEventCreateWithFlags(&c->ev_rdone[sl], hipEventDisableTiming));
+        HIPCHK(c, hipEventCreateWithFlags(&c->ev_adone[sl], hipEventDisableTiming));
+    }
+    const size_t need = (size_t)std::max(c->rows_local, 1) * (size_t)c->cfg.width * (size_t)n_frames * 3 * sizeof(float);
+    if (need <= c->slot_rgb_bytes[sl]) return PT_OK;
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->rstream[sl]));
+    (void)hipFree(c->slot_rgb[sl]);
+    c->slot_rgb[sl] = nullptr;
+    c->slot_rgb_bytes[sl] = 0;
+    HIPCHK(c, hipMalloc(&c->slot_rgb[sl], need));
+    c->slot_rgb_bytes[sl] = need;
     return PT_OK;
 }
 
@@ -1968,7 +2095,28 @@ static int enqueue_render(pt_ctx* c, int frame_first, int n_frames, int acc_firs
         const unsigned long long items = (unsigned long long)c->n_tiles * ng;
         p.grp_magic = (ng > 1 && items * ng < (1ull << 32)) ? (unsigned)(((1ull << 32) + ng - 1) / ng) : 0u;
     }
-    if (split_mode(c, n_frames, p.group)) {
+    // Overlapped short launches: a short frame-split render (the reference's one dispatch per
+    // displayed frame, ogl_path_trace.h:160-204) ends in a tail of nearly empty waves.  Its
+    // render kernel runs on overlap slot `sl` (own stream, colour scratch and queue counter)
+    // so the next render's waves fill the CUs that this one's tail frees; the accumulate pass
+    // stays on the main stream, in frame order (the running mean, :548-551).  Dependencies:
+    // the slot's scratch is reused only after the accumulate pass that read it (ev_adone), and
+    // a render never overlaps a tile-order sort (ev_sort; the sort runs on the main stream,
+    // which has waited for every earlier render).  Not for captured graphs or counting.
+    const bool overlap = c->overlap_slots > 1 && !frame_dev && !c->counting && n_frames <= kShortLaunch &&
+                         split_mode(c, n_frames, p.group);
+    const int sl = c->slot;
+    hipStream_t rs = c->stream;
+    unsigned* work = c->d_work;
+    if (overlap) {
+        int rc = ensure_slot(c, sl, n_frames);
+        if (rc) return rc;
+        rs = c->rstream[sl];
+        work = c->d_work + kQueueSet * (1 + sl);
+        p.rgb = c->slot_rgb[sl];
+        p.work_counter = work;
+        c->slot = (sl + 1) % c->overlap_slots;
+    } else if (split_mode(c, n_frames, p.group)) {
         int rc = ensure_rgb(c, n_frames);
         if (rc) return rc;
         p.rgb = c->d_rgb;
@@ -1979,7 +2127,11 @@ static int enqueue_render(pt_ctx* c, int frame_first, int n_frames, int acc_firs
     // variants: 0 state machine (default), 3 = 0 with the scene forced to stay in global memory
     const int variant = c->variant;
     const bool use_lds = variant == 0 && lds_staged(c);
-    HIPCHK(c, hipMemsetAsync(c->d_work, 0, sizeof(unsigned), c->stream));
+    if (overlap) {
+        if (c->adone_rec[sl]) HIPCHK(c, hipStreamWaitEvent(rs, c->ev_adone[sl], 0));
+        if (c->fence_rec) HIPCHK(c, hipStreamWaitEvent(rs, c->ev_fence, 0));
+    }
+    HIPCHK(c, hipMemsetAsync(work, 0, kQueueSet * sizeof(unsigned), rs));
     {
         // persistent grid: enough resident waves to fill every SIMD; surplus blocks find the
         // queue empty and exit.  Never more blocks than 8x8 tiles (64 lanes per tile).
@@ -2003,18 +2155,18 @@ static int enqueue_render(pt_ctx* c, int frame_first, int n_frames, int acc_firs
         p.shade_lds = shade_bytes <= 4096;
         const size_t top_lds = (size_t)p.n_top * 2 * sizeof(float4) + (p.shade_lds ? shade_bytes : 0);
 #define PT_LAUNCH_SM(L, M)                                                                                    \
-    if (c->counting && p.rgb) hipLaunchKernelGGL((k_render_sm<true, L, 5, M, true>), grid, dim3(256), L ? lds : top_lds, c->stream, p); \
-    else if (c->counting) hipLaunchKernelGGL((k_render_sm<true, L, 5, M, false>), grid, dim3(256), L ? lds : top_lds, c->stream, p); \
-    else if (p.rgb && mw == 8 && !M) hipLaunchKernelGGL((k_render_sm<false, L, 8, false, true>), grid, dim3(256), L ? lds : top_lds, c->stream, p); \
-    else if (p.rgb && mw == 7 && !M && L && c->walk_np == kPadNodes) hipLaunchKernelGGL((k_render_sm<false, true, 7, false, true, true>), grid, dim3(256), lds, c->stream, p); \
-    else if (p.rgb && mw == 7 && !M) hipLaunchKernelGGL((k_render_sm<false, L, 7, false, true>), grid, dim3(256), L ? lds : top_lds, c->stream, p); \
-    else if (p.rgb && mw >= 6) hipLaunchKernelGGL((k_render_sm<false, L, 6, M, true>), grid, dim3(256), L ? lds : top_lds, c->stream, p); \
-    else if (p.rgb) hipLaunchKernelGGL((k_render_sm<false, L, 5, M, true>), grid, dim3(256), L ? lds : top_lds, c->stream, p); \
-    else if (mw >= 6) hipLaunchKernelGGL((k_render_sm<false, L, 6, M, false>), grid, dim3(256), L ? lds : top_lds, c->stream, p); \
-    else hipLaunchKernelGGL((k_render_sm<false, L, 5, M, false>), grid, dim3(256), L ? lds : top_lds, c->stream, p);
+    if (c->counting && p.rgb) hipLaunchKernelGGL((k_render_sm<true, L, 5, M, true>), grid, dim3(256), L ? lds : top_lds, rs, p); \
+    else if (c->counting) hipLaunchKernelGGL((k_render_sm<true, L, 5, M, false>), grid, dim3(256), L ? lds : top_lds, rs, p); \
+    else if (p.rgb && mw == 8 && !M) hipLaunchKernelGGL((k_render_sm<false, L, 8, false, true>), grid, dim3(256), L ? lds : top_lds, rs, p); \
+    else if (p.rgb && mw == 7 && !M && L && c->walk_np == kPadNodes) hipLaunchKernelGGL((k_render_sm<false, true, 7, false, true, true>), grid, dim3(256), lds, rs, p); \
+    else if (p.rgb && mw == 7 && !M) hipLaunchKernelGGL((k_render_sm<false, L, 7, false, true>), grid, dim3(256), L ? lds : top_lds, rs, p); \
+    else if (p.rgb && mw >= 6) hipLaunchKernelGGL((k_render_sm<false, L, 6, M, true>), grid, dim3(256), L ? lds : top_lds, rs, p); \
+    else if (p.rgb) hipLaunchKernelGGL((k_render_sm<false, L, 5, M, true>), grid, dim3(256), L ? lds : top_lds, rs, p); \
+    else if (mw >= 6) hipLaunchKernelGGL((k_render_sm<false, L, 6, M, false>), grid, dim3(256), L ? lds : top_lds, rs, p); \
+    else hipLaunchKernelGGL((k_render_sm<false, L, 5, M, false>), grid, dim3(256), L ? lds : top_lds, rs, p);
 #define PT_LAUNCH_WIDE(NT, MW)                                                                                \
-    if (p.rgb) hipLaunchKernelGGL((k_render_sm<false, true, MW, false, true, false, NT>), grid, dim3(NT), lds, c->stream, p); \
-    else hipLaunchKernelGGL((k_render_sm<false, true, MW, false, false, false, NT>), grid, dim3(NT), lds, c->stream, p);
+    if (p.rgb) hipLaunchKernelGGL((k_render_sm<false, true, MW, false, true, false, NT>), grid, dim3(NT), lds, rs, p); \
+    else hipLaunchKernelGGL((k_render_sm<false, true, MW, false, false, false, NT>), grid, dim3(NT), lds, rs, p);
         // lds_threads: LDS scene, variant 0, one ray per pixel; the register budget of the
         // waves that are resident (6, 6, 4 per SIMD), not of 7
         if (nt > 256) {
@@ -2031,8 +2183,16 @@ static int enqueue_render(pt_ctx* c, int frame_first, int n_frames, int acc_firs
 #undef PT_LAUNCH_SM
         }
         if (p.rgb) {
+            if (overlap) {
+                HIPCHK(c, hipEventRecord(c->ev_rdone[sl], rs));
+                HIPCHK(c, hipStreamWaitEvent(c->stream, c->ev_rdone[sl], 0));
+            }
             long long px = (long long)c->rows_local * p.W;
             hipLaunchKernelGGL(k_accum_frames, dim3((unsigned)((px + 255) / 256)), dim3(256), 0, c->stream, p);
+            if (overlap) {
+                HIPCHK(c, hipEventRecord(c->ev_adone[sl], c->stream));
+                c->adone_rec[sl] = true;
+            }
         }
     }
     // The queue order is recomputed from the accumulated tile costs after every long launch,
@@ -2048,6 +2208,10 @@ static int enqueue_render(pt_ctx* c, int frame_first, int n_frames, int acc_firs
         c->order_sorted = true;
         hipLaunchKernelGGL(k_tile_order, dim3(1), dim3(1024), 0, c->stream, c->d_tile_cost, c->d_tile_perm,
                            c->n_tiles, c->tiles_x);
+        if (!frame_dev) {   // later overlapped renders start after the new order
+            HIPCHK(c, hipEventRecord(c->ev_fence, c->stream));
+            c->fence_rec = true;
+        }
     }
     HIPCHK(c, hipGetLastError());
     return PT_OK;
@@ -2185,6 +2349,8 @@ int pt_progressive_run(pt_ctx* c, int replays) {
     c->ev_pending.emplace_back(ev[0], ev[1]);
     HIPCHK(c, hipEventRecord(ev[0], c->stream));
     for (int r = 0; r < replays; r++) HIPCHK(c, hipGraphLaunch(c->graph_exec, c->stream));
+    HIPCHK(c, hipEventRecord(c->ev_fence, c->stream));   // the replays sort the tile order
+    c->fence_rec = true;
     HIPCHK(c, hipEventRecord(ev[1], c->stream));
     return PT_OK;
 }
@@ -2336,6 +2502,19 @@ int pt_stream(pt_ctx* c, void** s) {
     *s = (void*)c->stream;
     return PT_OK;
 }
+
+#ifdef PT_WAVE_TRACE
+extern "C" int pt_debug_wave_trace(unsigned long long* out, int max_waves, int reset) {
+    if (hipDeviceSynchronize() != hipSuccess) return -1;
+    const int n = max_waves < kWaveTraceMax ? max_waves : kWaveTraceMax;
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_wave_trace), sizeof(unsigned long long) * 4 * n) != hipSuccess) return -1;
+    if (reset) {
+        std::vector<unsigned long long> z(4 * (size_t)kWaveTraceMax, 0ull);
+        if (hipMemcpyToSymbol(HIP_SYMBOL(g_wave_trace), z.data(), z.size() * 8) != hipSuccess) return -1;
+    }
+    return n;
+}
+#endif
 
 #ifdef PT_PHASE_CLOCK
 extern "C" int pt_debug_phase_clock(unsigned long long out[8], int reset) {

@@ -171,7 +171,9 @@ int pt_viewer_frame(pt_viewer* v, pt_ctx* ctx, double now, pt_viewer_frame_info*
     int rc = pt_viewer_next(v, now, &info);
     if (!rc) rc = pt_set_display_mode(ctx, info.display_mode);
     if (!rc) rc = pt_set_camera(ctx, info.camera);
-    if (!rc) rc = pt_render(ctx, info.frame, 1, info.accumulate);
+    // enqueued like glDispatchCompute (ogl_path_trace.h:183): the host goes on to the next
+    // iteration while the GPU renders; readbacks and pt_sync wait for the frame
+    if (!rc) rc = pt_render_async(ctx, info.frame, 1, info.accumulate);
     if (out) *out = info;
     return rc;
 }

@@ -135,3 +135,60 @@ def test_budget_below_one_frame_still_renders(cornell_scene):
     xs, ys = rng.integers(0, W, 2000), rng.integers(0, Hh, 2000)
     want = O.render_pixels(cornell_scene, W, Hh, xs, ys, max_bounce=4, n_frames=5)
     assert_bitwise(got[ys, xs], want, "sub-frame budget")
+
+
+@pytest.mark.parametrize("overlap", [0, 1])
+def test_overlapped_short_launches_bitwise(cornell_scene, overlap):
+    """Short renders enqueued back to back (pt_render_async, no host wait) run their render
+    kernels on two alternating streams (tuning key 9), with the running mean applied in frame
+    order on the context's stream.  Mixed with a long launch, tile-order sorts (after the 8th
+    short launch, then every 64th), a graph replay and a reset: the oracle's image, on and
+    off."""
+    W, Hh = 64, 40
+    want = O.render(cornell_scene, W, Hh, max_bounce=8, n_frames=120)
+    pt = H.PathTracer(W, Hh, max_bounce=8)
+    pt.set_key(9, 0 if overlap else 1)
+    pt.upload(cornell_scene)
+    pt.write_rgba32f(np.full((Hh, W, 4), np.nan, np.float32))
+    f = 1
+    for _ in range(29):                          # frames 1..29, one per launch
+        pt.render_async(f, 1, 0 if f == 1 else 1)
+        f += 1
+    pt.render_async(f, 20, 1)                    # 30..49: a long launch on the main stream
+    f += 20
+    for n in [1, 2, 3, 1, 1] * 6:                # 50..97: short launches of 1-3 frames
+        pt.render_async(f, n, 1)
+        f += n
+    pt.sync()
+    mid = pt.read_rgba32f()
+    assert f == 98
+    pt.progressive_setup(frames_per_launch=2, launches_per_replay=2)
+    pt.progressive_reset(98)
+    pt.progressive_run(replays=2)                # 98..105 from the graph
+    for g in range(106, 121):                    # 106..120 overlapped again after the replay
+        pt.render_async(g, 1, 1)
+    got = pt.read_rgba32f()
+    pt.close()
+    want_mid = O.render(cornell_scene, W, Hh, max_bounce=8, n_frames=97)
+    assert_bitwise(mid, want_mid, "97 frames, overlap %d" % overlap)
+    assert_bitwise(got, want, "120 frames, overlap %d" % overlap)
+
+
+def test_overlapped_reset_and_camera_change(cornell_scene):
+    """The interactive loop's reset (ogl_path_trace.h:199-203): after a camera move the next
+    frame is frame 1 with accumulate = 0, enqueued while earlier frames may still render."""
+    W, Hh = 48, 32
+    cam2 = np.array([0.5, -5.5, 1.2, 0, 0.1, 1, 0, 0, 0, 0, 0, 0], np.float32)
+    sc2 = dict(cornell_scene)
+    sc2["cam"] = cam2
+    want = O.render(sc2, W, Hh, max_bounce=8, n_frames=12)
+    pt = H.PathTracer(W, Hh, max_bounce=8)
+    pt.upload(cornell_scene)
+    for f in range(1, 10):
+        pt.render_async(f, 1, 0 if f == 1 else 1)
+    pt.set_camera(cam2)
+    for f in range(1, 13):
+        pt.render_async(f, 1, 0 if f == 1 else 1)
+    got = pt.read_rgba32f()
+    pt.close()
+    assert_bitwise(got, want, "reset after camera move")

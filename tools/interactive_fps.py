@@ -1,8 +1,9 @@
-"""Interactive-loop rate with the image crossing PCIe every frame: the
-reference's render loop (one dispatch per displayed frame, ogl_path_trace.h:160-204) through
-pt_viewer_frame, each frame followed by the readback a window would upload -- the ACES RGBA8
-view (pt_read_rgba8_aces) or the raw RGBA32F accumulation.  Scene and accumulator stay in HBM;
-only the frame crosses to the host.  One GPU.
+"""Interactive-loop rate: the reference's render loop -- one dispatch per
+displayed frame, ogl_path_trace.h:160-204 -- through pt_viewer_frame (pt_render_async, like
+glDispatchCompute), with and without the per-frame readback a window would upload (the ACES
+RGBA8 view or the raw RGBA32F accumulation; a readback waits for its frame).  Each row is run
+with the overlapped short launches on (default) and off (tuning key 9).  Scene and accumulator
+stay in HBM.  One GPU.
 
 python tools/interactive_fps.py [--width 1920 --height 1080 --frames 300]
 """
@@ -25,6 +26,7 @@ def main():
     ap.add_argument("--frames", type=int, default=300)
     ap.add_argument("--bounces", type=int, default=8)
     ap.add_argument("--scene", default="cornell")
+    ap.add_argument("--rows", default="none,rgba8_aces,rgba32f")
     a = ap.parse_args()
     sb = H.setupBuffers(*pt_scenes.write_scene(a.scene, os.path.join(REPO, "scenes")))
     pt = H.PathTracer(a.width, a.height, max_bounce=a.bounces)
@@ -38,22 +40,26 @@ def main():
     pt.set_counting(False)
     out = {"width": a.width, "height": a.height, "bounces": a.bounces, "scene": a.scene, "frames": a.frames,
            "scene_upload_ms": round(upload_s * 1e3, 3), "segments_per_frame": seg_per_frame}
-    for readback in ("none", "rgba8_aces", "rgba32f"):
-        v = H.Viewer()
-        for i in range(10):                                   # warm-up
-            v.frame(pt, 0.001 * i)
-            pt.read_rgba8()
-        t0 = time.perf_counter()
-        for i in range(a.frames):
-            v.frame(pt, 1.0 + 0.001 * i)                      # pt_render is synchronous
-            if readback == "rgba8_aces":
-                pt.read_rgba8()
-            elif readback == "rgba32f":
-                pt.read_rgba32f()
-        dt = time.perf_counter() - t0
-        v.close()
-        out[readback] = {"ms_per_frame": round(dt * 1e3 / a.frames, 4), "fps": round(a.frames / dt, 1),
-                         "mrays_per_s": round(seg_per_frame * a.frames / dt / 1e6, 1)}
+    for overlap in (1, 0):
+        pt.set_key(9, 0 if overlap else 1)
+        for readback in a.rows.split(","):
+            v = H.Viewer()
+            for i in range(70):                               # warm-up (and the first tile sorts)
+                v.frame(pt, 0.001 * i)
+            pt.sync()
+            t0 = time.perf_counter()
+            for i in range(a.frames):
+                v.frame(pt, 1.0 + 0.001 * i)                  # enqueued, like glDispatchCompute
+                if readback == "rgba8_aces":
+                    pt.read_rgba8()
+                elif readback == "rgba32f":
+                    pt.read_rgba32f()
+            pt.sync()
+            dt = time.perf_counter() - t0
+            v.close()
+            out["%s%s" % (readback, "" if overlap else "_no_overlap")] = {
+                "ms_per_frame": round(dt * 1e3 / a.frames, 4), "fps": round(a.frames / dt, 1),
+                "mrays_per_s": round(seg_per_frame * a.frames / dt / 1e6, 1)}
     pt.close()
     print(json.dumps(out))
 
