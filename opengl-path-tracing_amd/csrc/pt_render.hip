@@ -1268,7 +1268,7 @@ struct pt_ctx {
     float root_box[6] = {0, 0, 0, 0, 0, 0};
     int root_child = -1;
     // the tree is a full binary tree threaded in preorder whose internal boxes contain their
-    // children's (nested_tree): the LDS walk may cull with slab_oct_cons (tuning key 15 = 1: off)
+    // children's (pt_bvh_culling_ok): the LDS walk may cull with slab_oct_cons (tuning key 15 = 1: off)
     bool walk_nested = false;
     int cons_off = 0;
     float cons_m[3] = {0, 0, 0};   // KParams::cons_m
@@ -1338,51 +1338,6 @@ static int fail(pt_ctx* c, int code, const std::string& msg) {
         if (e_ != hipSuccess)                                                               \
             return fail(ctx, PT_E_HIP, std::string(#call ": ") + hipGetErrorString(e_));     \
     } while (0)
-
-// The structure the culling walk relies on, on the std140 records: from
-// the root, a full binary tree threaded in preorder -- an internal node's hit link is its
-// left child L, L's miss link its right child R, R's miss link the node's own -- in which
-// every internal box contains both children's boxes (exact float compares).  A walk that
-// enters a subtree the exact test would skip then leaves it at the same miss link, and any
-// leaf inside has a box within the skipped one, which fails the exact test too.
-// A link field as a node index: finite, integral and in [-1, n_nodes), else -2 (never a
-// valid link; casting NaN or a huge float to int would be undefined behaviour).
-static int link_of(float v, int n_nodes) {
-    if (!(v >= -1.0f && v < (float)n_nodes) || v != (float)(int)v) return -2;
-    return (int)v;
-}
-
-static bool nested_tree(const float* bvh, int n_nodes) {
-    if (n_nodes <= 0) return false;
-    std::vector<unsigned char> seen(n_nodes, 0);
-    std::vector<std::pair<int, int>> st;   // (node, the miss link it must carry)
-    st.emplace_back(0, -1);
-    while (!st.empty()) {
-        const int x = st.back().first, after = st.back().second;
-        st.pop_back();
-        if (x < 0 || x >= n_nodes || seen[x]) return false;
-        seen[x] = 1;
-        const float* nd = bvh + 12 * (size_t)x;
-        const int hit = link_of(nd[10], n_nodes), miss = link_of(nd[11], n_nodes);
-        if (hit == -2 || miss != after) return false;
-        if (nd[8] > -1.0f) {                       // leaf: its hit link is its miss link
-            if (hit != miss) return false;
-            continue;
-        }
-        const int l = hit;
-        if (l < 0) return false;
-        const int r = link_of(bvh[12 * (size_t)l + 11], n_nodes);
-        if (r < 0 || r == after) return false;
-        for (int ch : {l, r}) {
-            const float* cb = bvh + 12 * (size_t)ch;
-            for (int q = 0; q < 3; q++)
-                if (!(nd[q] <= cb[q] && cb[4 + q] <= nd[4 + q])) return false;
-        }
-        st.emplace_back(r, after);
-        st.emplace_back(l, r);
-    }
-    return true;
-}
 
 static void free_scene(pt_ctx* c) {
     (void)hipFree(c->d_nodes); (void)hipFree(c->d_tris); (void)hipFree(c->d_mats); (void)hipFree(c->d_spheres);
@@ -1480,10 +1435,6 @@ void pt_destroy(pt_ctx* c) {
 }
 
 const char* pt_last_error(const pt_ctx* c) { return c ? c->err.c_str() : "null context"; }
-
-int pt_bvh_culling_ok(const float* nodes, int n_nodes) {
-    return nodes && n_nodes > 0 && nested_tree(nodes, n_nodes) ? 1 : 0;
-}
 
 int pt_upload_scene(pt_ctx* c, const float* tris, int n_tris, const float* bvh, int n_nodes,
                     const float* mats, int n_mats, const float* spheres, int n_spheres) {
@@ -1672,7 +1623,7 @@ int pt_upload_scene(pt_ctx* c, const float* tris, int n_tris, const float* bvh, 
     // walks while its position lies below the sink image.  A leaf's coplanar flag moves to
     // slot 2k+1 quad 1 .w (the sink index carries only k).
     std::vector<float4> dsk;
-    const bool nested = nested_tree(bvh, n_nodes);
+    const bool nested = pt_bvh_culling_ok(bvh, n_nodes) == 1;   // pt_scene.cpp
     if (nested) {
         dsk.assign(18 * N, make_float4(0, 0, 0, 0));
         std::copy(dwl.begin(), dwl.end(), dsk.begin());

@@ -642,6 +642,55 @@ namespace pt_internal {
 void set_bvh_error(const std::string& msg) { g_bvh_err = msg; }
 }
 
+namespace {
+
+// The structure the culling walk relies on, on the std140 records: from
+// the root, a full binary tree threaded in preorder -- an internal node's hit link is its
+// left child L, L's miss link its right child R, R's miss link the node's own -- in which
+// every internal box contains both children's boxes (exact float compares).  A walk that
+// enters a subtree the exact test would skip then leaves it at the same miss link, and any
+// leaf inside has a box within the skipped one, which fails the exact test too.
+// A link field as a node index: finite, integral and in [-1, n_nodes), else -2 (never a
+// valid link; casting NaN or a huge float to int would be undefined behaviour).
+static int link_of(float v, int n_nodes) {
+    if (!(v >= -1.0f && v < (float)n_nodes) || v != (float)(int)v) return -2;
+    return (int)v;
+}
+
+static bool nested_tree(const float* bvh, int n_nodes) {
+    if (n_nodes <= 0) return false;
+    std::vector<unsigned char> seen(n_nodes, 0);
+    std::vector<std::pair<int, int>> st;   // (node, the miss link it must carry)
+    st.emplace_back(0, -1);
+    while (!st.empty()) {
+        const int x = st.back().first, after = st.back().second;
+        st.pop_back();
+        if (x < 0 || x >= n_nodes || seen[x]) return false;
+        seen[x] = 1;
+        const float* nd = bvh + 12 * (size_t)x;
+        const int hit = link_of(nd[10], n_nodes), miss = link_of(nd[11], n_nodes);
+        if (hit == -2 || miss != after) return false;
+        if (nd[8] > -1.0f) {                       // leaf: its hit link is its miss link
+            if (hit != miss) return false;
+            continue;
+        }
+        const int l = hit;
+        if (l < 0) return false;
+        const int r = link_of(bvh[12 * (size_t)l + 11], n_nodes);
+        if (r < 0 || r == after) return false;
+        for (int ch : {l, r}) {
+            const float* cb = bvh + 12 * (size_t)ch;
+            for (int q = 0; q < 3; q++)
+                if (!(nd[q] <= cb[q] && cb[4 + q] <= nd[4 + q])) return false;
+        }
+        st.emplace_back(r, after);
+        st.emplace_back(l, r);
+    }
+    return true;
+}
+
+}  // namespace
+
 extern "C" {
 
 const char* pt_bvh_last_error(void) { return g_bvh_err.c_str(); }
@@ -768,6 +817,10 @@ void pt_aces_rgba8_host(const float* rgba, long long n, unsigned char* out) {
         }
         out[4 * i + 3] = 255;
     }
+}
+
+int pt_bvh_culling_ok(const float* nodes, int n_nodes) {
+    return nodes && n_nodes > 0 && nested_tree(nodes, n_nodes) ? 1 : 0;
 }
 
 }  // extern "C"

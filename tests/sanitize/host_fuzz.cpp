@@ -1,0 +1,234 @@
+// host_fuzz.cpp -- ASan + UBSan driver for the host-side ingest of the drop-in library
+// (csrc/pt_scene.cpp, csrc/pt_viewer.cpp): the OBJ/MTL loaders (reference and robust modes,
+// geometry_loader.h:15-142), the SAH builder (bvh.h:173-268), the culling-walk tree check and
+// the headless viewer controller (ogl_path_trace.h:258-364).  Test infrastructure only: built
+// by tests/sanitize/Makefile with -fsanitize=address,undefined -fno-sanitize-recover, run by
+// tests/test_sanitize.py; any report aborts the process.
+//
+// usage: host_fuzz <scratch_dir> <iterations> [obj mtl]...
+//   every (obj, mtl) pair is loaded in both modes and built; then <iterations> mutated OBJ/MTL
+//   texts (deterministic seed) go through both loaders, and random node arrays through
+//   pt_bvh_culling_ok.  Prints one summary line; exit 0 = no crash and every call returned a
+//   defined status.
+#include "../../include/pt_api.h"
+#include "../../include/pt_scene.h"
+#include "../../include/pt_viewer.h"
+
+#include <cmath>
+#include <cstdint>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <string>
+#include <vector>
+
+// The GPU entry points pt_scene.cpp / pt_viewer.cpp reference, as refusing stubs: this
+// binary is host-only (no HIP runtime linked).
+extern "C" {
+int pt_bvh_build_gpu(const float*, int, float*, int, int*, int) { return PT_E_HIP; }
+int pt_render_async(pt_ctx*, int, int, int) { return PT_E_HIP; }
+int pt_set_camera(pt_ctx*, const float*) { return PT_E_HIP; }
+int pt_set_display_mode(pt_ctx*, int) { return PT_E_HIP; }
+}
+
+namespace {
+
+uint64_t g_rng = 0x5EEDF00Dull;
+uint32_t rnd() {
+    g_rng = g_rng * 6364136223846793005ull + 1442695040888963407ull;
+    return (uint32_t)(g_rng >> 33);
+}
+
+bool write_file(const std::string& path, const std::string& text) {
+    FILE* f = std::fopen(path.c_str(), "wb");
+    if (!f) return false;
+    std::fwrite(text.data(), 1, text.size(), f);
+    std::fclose(f);
+    return true;
+}
+
+std::string read_file(const char* path) {
+    std::string s;
+    FILE* f = std::fopen(path, "rb");
+    if (!f) return s;
+    char buf[65536];
+    size_t n;
+    while ((n = std::fread(buf, 1, sizeof buf, f)) > 0) s.append(buf, n);
+    std::fclose(f);
+    return s;
+}
+
+int g_ok = 0, g_err = 0;
+
+// Load (both modes), add built-ins, build, copy out, check the tree; every status must be
+// 0 or a PT_E* code.
+void exercise(const char* obj, const char* mtl) {
+    for (int mode = 0; mode < 2; mode++) {
+        pt_scene* s = nullptr;
+        int rc = pt_scene_load_obj_ex(obj, mtl, mode, &s);
+        if (rc > 0 || rc < -16) { std::fprintf(stderr, "bad status %d\n", rc); std::abort(); }
+        if (rc != 0) {
+            g_err++;
+            if (s) pt_scene_free(s);
+            continue;
+        }
+        g_ok++;
+        pt_scene_add_builtins(s);
+        pt_scene_add_builtins(s);   // idempotent
+        int cnt[5] = {0, 0, 0, 0, 0};
+        if (pt_scene_counts(s, cnt) == 0 && cnt[0] > 0 && cnt[0] < (1 << 16)) {
+            if (pt_scene_build_bvh(s) == 0) {
+                pt_scene_counts(s, cnt);
+                std::vector<float> nodes((size_t)cnt[3] * 12), tris((size_t)cnt[0] * 16);
+                pt_scene_get_nodes(s, nodes.data(), cnt[3]);
+                pt_scene_get_tris(s, tris.data(), cnt[0]);
+                pt_bvh_culling_ok(nodes.data(), cnt[3]);
+                std::vector<float> n2((size_t)(2 * cnt[0]) * 12);
+                int nn = 0;
+                pt_bvh_build(tris.data(), cnt[0], n2.data(), 2 * cnt[0], &nn);
+                if (nn != cnt[3] || std::memcmp(n2.data(), nodes.data(), (size_t)nn * 48) != 0) {
+                    std::fprintf(stderr, "pt_bvh_build differs from pt_scene_build_bvh\n");
+                    std::abort();
+                }
+                // too small a capacity must be an error, not an overflow
+                if (cnt[0] > 1 && pt_bvh_build(tris.data(), cnt[0], n2.data(), cnt[3] - 1, &nn) == 0) {
+                    std::fprintf(stderr, "undersized node buffer accepted\n");
+                    std::abort();
+                }
+            }
+            std::vector<float> mats((size_t)cnt[1] * 16), sph((size_t)std::max(cnt[2], 1) * 8);
+            pt_scene_get_mats(s, mats.data(), cnt[1]);
+            pt_scene_get_spheres(s, sph.data(), cnt[2]);
+        }
+        (void)pt_scene_last_error(s);
+        pt_scene_free(s);
+    }
+}
+
+const char* kTokens[] = {"v", "f", "vt", "vn", "usemtl", "newmtl", "mtllib", "Kd", "Ke", "Ks", "Ns", "#",
+                         "-1", "0", "1", "2", "3", "-2147483648", "2147483647", "99999999999", "nan",
+                         "inf", "-inf", "1e39", "1e-45", "/", "//", "1/2/3", "\\", "\t", " ", "\n",
+                         "\r\n", "o", "g", "s off", "\xff\xfe", "0x1p3", "+", "-", "."};
+
+std::string mutate(const std::string& base) {
+    std::string s = base;
+    const int edits = 1 + (int)(rnd() % 8);
+    for (int e = 0; e < edits; e++) {
+        const size_t pos = s.empty() ? 0 : rnd() % (s.size() + 1);
+        switch (rnd() % 6) {
+        case 0:   // flip a byte
+            if (!s.empty()) s[pos % s.size()] = (char)(rnd() & 0xff);
+            break;
+        case 1:   // insert a token
+            s.insert(pos, kTokens[rnd() % (sizeof kTokens / sizeof kTokens[0])]);
+            break;
+        case 2:   // delete a run
+            if (!s.empty()) s.erase(pos % s.size(), 1 + rnd() % 16);
+            break;
+        case 3:   // truncate
+            s.resize(pos);
+            break;
+        case 4:   // a long line (the reference's reader assumes < 128 characters)
+            s.insert(pos, std::string(100 + rnd() % 400, "v 1 "[rnd() % 4]));
+            break;
+        default:  // duplicate a line
+            if (!s.empty()) {
+                size_t a = s.rfind('\n', pos % s.size());
+                a = a == std::string::npos ? 0 : a + 1;
+                size_t b = s.find('\n', a);
+                s.insert(pos, s.substr(a, b == std::string::npos ? std::string::npos : b - a + 1));
+            }
+            break;
+        }
+    }
+    return s;
+}
+
+// Random node arrays: garbage links, NaNs, huge values, partial trees.
+void fuzz_nodes(int iters) {
+    for (int it = 0; it < iters; it++) {
+        const int n = 1 + (int)(rnd() % 40);
+        std::vector<float> nd((size_t)n * 12);
+        for (auto& x : nd) {
+            switch (rnd() % 8) {
+            case 0: x = NAN; break;
+            case 1: x = INFINITY; break;
+            case 2: x = 3e38f; break;
+            case 3: x = -1.0f; break;
+            case 4: x = (float)(rnd() % (unsigned)(n + 2)) - 1.0f; break;
+            case 5: x = 0.5f; break;
+            default: x = (float)(int)(rnd() % 64) - 8.0f; break;
+            }
+        }
+        const int r = pt_bvh_culling_ok(nd.data(), n);
+        if (r != 0 && r != 1) std::abort();
+    }
+}
+
+void fuzz_viewer(int iters) {
+    pt_viewer* v = nullptr;
+    if (pt_viewer_create(nullptr, 1, &v) != 0) std::abort();
+    const int keys[] = {PT_KEY_SPACE, PT_KEY_1, PT_KEY_2, PT_KEY_3, PT_KEY_4, PT_KEY_A, PT_KEY_D, PT_KEY_S,
+                        PT_KEY_W, PT_KEY_LEFT_SHIFT, -1, 0, 1 << 20};
+    double now = 0.0;
+    for (int it = 0; it < iters; it++) {
+        pt_viewer_key(v, keys[rnd() % (sizeof keys / sizeof keys[0])], (int)(rnd() % 4) - 0);
+        const double cx = (rnd() % 3 == 0) ? 1e300 * ((rnd() & 1) ? 1 : -1) : (double)(int)(rnd() % 4000) - 2000.0;
+        pt_viewer_cursor(v, cx, (double)(int)(rnd() % 4000) - 2000.0);
+        now += (rnd() % 5 == 0) ? -1.0 : 0.016;
+        pt_viewer_frame_info fi;
+        pt_viewer_next(v, now, &fi);
+        if (pt_viewer_frame(v, nullptr, now, nullptr) == 0) std::abort();   // null ctx / stubs refuse
+        (void)pt_viewer_should_close(v);
+    }
+    pt_viewer_set_params(v, 1e30f, -1e30f, 0);
+    pt_viewer_frame_info fi;
+    pt_viewer_next(v, now + 1.0, &fi);
+    pt_viewer_destroy(v);
+}
+
+}  // namespace
+
+int main(int argc, char** argv) {
+    if (argc < 3) {
+        std::fprintf(stderr, "usage: %s <scratch_dir> <iterations> [obj mtl]...\n", argv[0]);
+        return 2;
+    }
+    const std::string dir = argv[1];
+    const int iters = std::atoi(argv[2]);
+    std::vector<std::pair<std::string, std::string>> seeds;
+    for (int i = 3; i + 1 < argc; i += 2) {
+        exercise(argv[i], argv[i + 1]);
+        seeds.emplace_back(read_file(argv[i]), read_file(argv[i + 1]));
+    }
+    if (seeds.empty()) seeds.emplace_back("v 0 0 0\nv 1 0 0\nv 0 1 0\nusemtl a\nf 1 2 3\n",
+                                          "newmtl a\nKd 1 1 1\nKe 0 0 0\nKs 0 0 0\nNs 10\nNi 1\nd 1\nillum 2\nx\n");
+    const std::string obj = dir + "/fz.obj", mtl = dir + "/fz.mtl";
+    for (int it = 0; it < iters; it++) {
+        const auto& sd = seeds[rnd() % seeds.size()];
+        // small seeds stay whole; large ones are cut to a prefix so an iteration stays cheap
+        std::string o = sd.first.size() > 4096 ? sd.first.substr(0, 4096) : sd.first;
+        std::string m = sd.second;
+        if (rnd() & 1) o = mutate(o);
+        else m = mutate(m);
+        if (!write_file(obj, o) || !write_file(mtl, m)) return 3;
+        exercise(obj.c_str(), mtl.c_str());
+        if (it % 7 == 0) {   // mtllib resolution (robust mode, mtl_path NULL)
+            pt_scene* s = nullptr;
+            if (pt_scene_load_obj_ex(obj.c_str(), nullptr, PT_LOAD_ROBUST, &s) == 0) g_ok++;
+            if (s) pt_scene_free(s);
+        }
+    }
+    // the missing-file and null-argument paths
+    pt_scene* s = nullptr;
+    if (pt_scene_load_obj((dir + "/missing.obj").c_str(), mtl.c_str(), &s) == 0) return 4;
+    if (s) pt_scene_free(s);
+    if (pt_scene_from_arrays(nullptr, 1, nullptr, 0, &s) == 0) return 4;
+    fuzz_nodes(iters * 4);
+    fuzz_viewer(iters);
+    std::vector<float> px = {0.f, 1.f, NAN, INFINITY, -1.f, 1e30f, 0.5f, 2.f};
+    unsigned char out[8];
+    pt_aces_rgba8_host(px.data(), 2, out);
+    std::printf("host_fuzz ok: %d loads accepted, %d rejected, %d iterations\n", g_ok, g_err, iters);
+    return 0;
+}
