@@ -27,6 +27,7 @@ def main():
     ap.add_argument("--bounces", type=int, default=8)
     ap.add_argument("--scene", default="cornell")
     ap.add_argument("--rows", default="none,rgba8_aces,rgba32f")
+    ap.add_argument("--slots", default="0,1", help="tuning key 9 values: 0 = automatic, 1 = no overlap, 2..4")
     a = ap.parse_args()
     sb = H.setupBuffers(*pt_scenes.write_scene(a.scene, os.path.join(REPO, "scenes")))
     pt = H.PathTracer(a.width, a.height, max_bounce=a.bounces)
@@ -40,8 +41,9 @@ def main():
     pt.set_counting(False)
     out = {"width": a.width, "height": a.height, "bounces": a.bounces, "scene": a.scene, "frames": a.frames,
            "scene_upload_ms": round(upload_s * 1e3, 3), "segments_per_frame": seg_per_frame}
-    for overlap in (1, 0):
-        pt.set_key(9, 0 if overlap else 1)
+    for slots in (int(x) for x in a.slots.split(",")):
+        pt.set_key(9, slots)
+        suffix = "" if slots == 0 else ("_no_overlap" if slots == 1 else "_slots%d" % slots)
         for readback in a.rows.split(","):
             v = H.Viewer()
             for i in range(70):                               # warm-up (and the first tile sorts)
@@ -57,7 +59,7 @@ def main():
             pt.sync()
             dt = time.perf_counter() - t0
             v.close()
-            out["%s%s" % (readback, "" if overlap else "_no_overlap")] = {
+            out[readback + suffix] = {
                 "ms_per_frame": round(dt * 1e3 / a.frames, 4), "fps": round(a.frames / dt, 1),
                 "mrays_per_s": round(seg_per_frame * a.frames / dt / 1e6, 1)}
     pt.close()
