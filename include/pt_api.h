@@ -157,13 +157,11 @@ int pt_set_kernel(pt_ctx* ctx, int variant);
  *         A render whose per-frame colours (12 B per pixel-frame) exceed it -- or whose
  *         32-bit work-queue ids would overflow -- runs as back-to-back launches, the first
  *         with the caller's accumulate flag and the rest accumulating: the same image.
- * key 9 = overlapped short launches: render slots 2..4, 1 = off, 0 = automatic (3).  Renders
+ * key 9 = overlapped short launches: render slots 2..4, 1 = off, 0 = automatic (2).  Renders
  *         of at most 16 frames (the reference's one dispatch per displayed frame) run their
  *         render kernel on one of these extra streams, so the next render fills the CUs that
  *         this one's launch tail frees; the running mean is still applied on the context's
  *         stream in frame order.
- * key 10 = work-queue heads of frame-split launches (1..8; 0 = automatic: 8 for renders of at
- *         most 16 frames, whose pulls would saturate one device-scope counter, else 1).
  * key 15 = culling walk (0 = automatic, 1 = off).  When the uploaded tree is a full binary
  *         tree threaded in preorder whose internal boxes contain their children's, the
  *         LDS-staged walk tests nodes with a cheaper conservative slab test and re-tests a

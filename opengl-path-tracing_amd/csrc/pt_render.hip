@@ -66,7 +66,6 @@ struct KParams {
     int trav_floor;                // ... and the walk floor: fewer walking lanes end a walk phase
     int compact_max;               // leaf phase: compact the edge tests of at most this many pairs (<= 63)
     int pull_batch;                // frame-split mode: queue ids a wave reserves per queue atomic (>= 32)
-    int n_shards;                  // frame-split mode: work-queue heads (1..kShards)
     unsigned* reset_work;          // k_accum_frames zeroes these queue heads (an overlap slot's) for its next use
     const int* frame_dev;          // progressive graph: device frame counter (null = use frame_first)
     int frame_offset;              // this launch's frame offset from *frame_dev
@@ -524,12 +523,9 @@ __device__ __forceinline__ void leaf_pair_tests(const SceneView& S, bool at, int
 // =====================================================================================
 enum : int { ST_DONE = 0, ST_TRAV = 1, ST_LEAF = 2, ST_SHADE = 3 };
 constexpr unsigned kPullBatch = 32;
-// frame-split work queue: up to kShards heads (KParams::n_shards), kShardStride unsigned apart
-// (own 128-B lines)
-#ifndef PT_SHARDS
-#define PT_SHARDS 8
-#endif
-constexpr int kShards = PT_SHARDS, kShardStride = 32;
+// work-queue head stride (unsigned): each context stream / overlap slot has its own head on
+// its own 128-B line
+constexpr int kQueueStride = 32;
 #ifndef PT_WALK_UNROLL
 #define PT_WALK_UNROLL 4
 #endif
@@ -670,10 +666,7 @@ constexpr int kWaveTraceMax = 16384;
 __device__ unsigned long long g_wave_trace[kWaveTraceMax * 4];
 #endif
 
-// SHARD: the frame-split queue has p.n_shards heads (short launches); a separate instantiation,
-// so the one-head kernel of long launches keeps its own code generation (the sharded pull path
-// in the one kernel cost 5% on C2's 1024-frame launch)
-template <bool COUNT, bool LDS, int MINW, bool MULTI, bool SPLIT, bool PADN = false, int NT = 256, bool SHARD = false>
+template <bool COUNT, bool LDS, int MINW, bool MULTI, bool SPLIT, bool PADN = false, int NT = 256>
 __global__ __launch_bounds__(NT, MINW) void k_render_sm(KParams p) {
 #ifdef PT_WAVE_TRACE
     const unsigned long long wt_entry = __builtin_amdgcn_s_memrealtime();
@@ -736,7 +729,6 @@ __global__ __launch_bounds__(NT, MINW) void k_render_sm(KParams p) {
     const int tiles_x = (p.W + 7) >> 3;
     const unsigned n_groups = SPLIT ? (unsigned)((p.n_frames + p.group - 1) / p.group) : 1u;
     const unsigned total_ids = (unsigned)tiles_x * (unsigned)((p.rows_local + 7) >> 3) * n_groups * 64u;
-    const unsigned n_items = total_ids >> 6;
     const int n_nodes = p.sc.n_nodes;
     const bool use_tris = !(p.flags & PT_FLAG_NO_TRIANGLES) && n_nodes > 0;
     // walk start for a ray inside the root box: its first child (the counting build walks
@@ -754,8 +746,6 @@ __global__ __launch_bounds__(NT, MINW) void k_render_sm(KParams p) {
     int aidx = 0;             // rows_local * W < 2^31 (checked at pt_create)
     int k = 0, kend = 0, r = 0, bounce = 0;   // frames k..kend-1 of this work item
     unsigned qnext = 0, qend = 0;             // wave's reserved queue ids (frame-split mode)
-    const unsigned n_shards = SHARD ? (unsigned)p.n_shards : 1u;
-    unsigned qshard = SHARD ? blockIdx.x % n_shards : 0u, qtried = 0;   // its shard; shards found dry in a row
     unsigned tile_id = 0, pcost = 0;    // adaptive queue order: this pixel's tile + segments
     float4 acc = make_float4(0, 0, 0, 0);
     f3 psum = mk(0, 0, 0), o = mk(0, 0, 0), d = mk(0, 0, 1), inc = mk(0, 0, 0), col = mk(1, 1, 1);
@@ -889,12 +879,9 @@ __global__ __launch_bounds__(NT, MINW) void k_render_sm(KParams p) {
             }
             // wave-aggregated pull from the work queue.  Frame-split items are short, so
             // there a wave reserves ids in batches of pull_batch (one queue atomic per batch
-            // instead of per pull).  SHARD: the queue is sharded (n_shards heads, shard s owns
-            // items s, s + n_shards, ...: each shard keeps the expensive-first tile order): one
-            // device-scope head saturates near 88 dequeues per microsecond, which bounded the
-            // one-frame launches.  A wave starts on shard blockIdx mod n_shards (its XCD) and
-            // moves on when that shard runs dry; it is done once it has found n_shards shards
-            // dry in a row.  Register mode keeps one head (long items, few pulls).
+            // instead of per pull; the counter is one address for the whole chip).  (A queue
+            // sharded over 8 heads, one per XCD, measured slower on one-frame launches with
+            // and without overlap, and cost 5% on C2 in the same kernel.)
             bool want = st == ST_SHADE && lx < 0;
             unsigned long long m = __ballot(want);
             if (m) {
@@ -902,32 +889,9 @@ __global__ __launch_bounds__(NT, MINW) void k_render_sm(KParams p) {
                 const unsigned rank = (unsigned)rank_in(m);
                 const int leader = __ffsll((long long)m) - 1;
                 unsigned id;
-                bool valid = true;
-                const unsigned sh = qshard;
                 if (SPLIT && qend - qnext >= need) {
                     id = qnext + rank;
                     qnext += need;
-                    qtried = 0;
-                    // a sharded reservation ends at its shard's last id; the one-head queue's
-                    // may run past the queue's end
-                    if (!SHARD) valid = id < total_ids;
-                } else if (SHARD) {
-                    const unsigned shard_ids = ((n_items + (n_shards - 1u) - sh) / n_shards) * 64u;
-                    const unsigned avail = qend - qnext;
-                    const unsigned take = max(need - avail, (unsigned)p.pull_batch);
-                    unsigned base = 0;
-                    if (want && rank == 0u) base = atomicAdd(p.work_counter + kShardStride * sh, take);   // the leader
-                    base = (unsigned)__builtin_amdgcn_readlane((int)base, leader);
-                    id = rank < avail ? qnext + rank : base + (rank - avail);
-                    valid = id < shard_ids;
-                    qnext = base + (need - avail);
-                    qend = base + take < shard_ids ? base + take : shard_ids;
-                    // shards found dry with lanes left unserved, in a row
-                    qtried = qnext <= shard_ids ? 0u : qtried + 1u;
-                    if (qnext >= qend) {       // this shard ran dry: the next one
-                        qnext = qend = 0u;
-                        qshard = sh + 1u == n_shards ? 0u : sh + 1u;
-                    }
                 } else {
                     const unsigned avail = SPLIT ? qend - qnext : 0u;
                     const unsigned take = SPLIT ? max(need - avail, (unsigned)p.pull_batch) : need;
@@ -935,19 +899,16 @@ __global__ __launch_bounds__(NT, MINW) void k_render_sm(KParams p) {
                     if (want && rank == 0u) base = atomicAdd(p.work_counter, take);   // the leader
                     base = (unsigned)__builtin_amdgcn_readlane((int)base, leader);
                     id = rank < avail ? qnext + rank : base + (rank - avail);
-                    valid = id < total_ids;
                     if (SPLIT) {
                         qnext = base + (need - avail);
                         qend = base + take;
                     }
                 }
                 if (want) {
-                    if (!valid) {
-                        // register mode: the queue is empty; split mode: empty once every
-                        // shard has been found dry, else retry on the next shard
-                        if (!SHARD || qtried >= n_shards) st = ST_DONE;
+                    if (id >= total_ids) {
+                        st = ST_DONE;
                     } else {
-                        const unsigned item = SHARD ? (id >> 6) * n_shards + sh : id >> 6, w = id & 63u;
+                        const unsigned item = id >> 6, w = id & 63u;
                         // item -> (tile, frame group): by the host's exact magic reciprocal
                         // (kernel argument) when it is valid for every item
                         unsigned tile = item;
@@ -1199,7 +1160,7 @@ __global__ __launch_bounds__(256) void k_accum_frames(KParams p) {
     resolve_frames(p);
     // the render that used these queue heads has ended (this pass runs after it): ready them
     // for the slot's next render, which waits for this pass (no fill dispatch per launch)
-    if (p.reset_work && blockIdx.x == 0 && threadIdx.x < (unsigned)(kShards * kShardStride)) p.reset_work[threadIdx.x] = 0u;
+    if (p.reset_work && blockIdx.x == 0 && threadIdx.x == 0) *p.reset_work = 0u;
     const long long n = (long long)p.rows_local * p.W;
     const long long idx = (long long)blockIdx.x * blockDim.x + threadIdx.x;
     if (idx >= n) return;
@@ -1251,11 +1212,12 @@ constexpr size_t kLdsSceneSmall = 48 * 1024;  // staged by 256-thread workgroups
 // staged in LDS, 24 KiB per workgroup (6 workgroups per CU stay resident)
 constexpr int kTopNodes = 768;
 // overlapped short launches: render slots (tuning key 9).  A slot's scratch is reused only
-// after the accumulate pass that read it, and that pass gets CUs only as render blocks retire,
-// so with 2 slots render f+1 waited for the end of render f (measured 0.61 ms per 1080p frame);
-// with 3 it waits only for render f-1.
-constexpr int kMaxSlots = 4, kAutoSlots = 3;
-constexpr size_t kQueueSet = (size_t)kShards * kShardStride;   // unsigned per set of queue heads
+// after the accumulate pass that read it.  Measured on 1080p Cornell one-frame launches (ms per
+// frame): 1 slot (no overlap) 0.80, 2 slots 0.60, 3 slots 0.62, 4 slots 0.66 -- more slots
+// put more renders in flight, whose blocks then hold the CUs longer before the accumulate
+// passes (and with them the slots) come free.
+constexpr int kMaxSlots = 4, kAutoSlots = 2;
+constexpr size_t kQueueSet = kQueueStride;   // unsigned per queue head
 
 struct pt_ctx {
     pt_config cfg{};
@@ -1302,7 +1264,6 @@ struct pt_ctx {
     // made a walk step cheaper; re-swept with the sink walk: 5 +0.9% over 3, 2-8 within 1%)
     // (+0.8% on C2, +0.5% on C3 over no floor) -- tools/probe.py sweeps
     int leaf_thresh = 0, shade_thresh = 0, minw = 0, trav_floor = 0, compact_max = 63, pull_batch = 0;
-    int shards = 0;                 // tuning key 10: frame-split queue heads (0 = automatic)
     // frame-split work items (KParams::group): 0 = automatic, n = frames per item
     int group_force = 0;
     int n_cu = 0;
@@ -1401,7 +1362,7 @@ int pt_create(const pt_config* cfg, pt_ctx** out) {
     HIPCHK(c, hipMemset(c->accum, 0, std::max<size_t>(px, 1) * sizeof(float4)));
     HIPCHK(c, hipMalloc(&c->rgba8, std::max<size_t>(px, 1) * sizeof(uchar4)));
     HIPCHK(c, hipMalloc(&c->d_counters, 16 * sizeof(unsigned long long)));
-    // work-queue heads: one set of kShards heads (kShardStride apart) for the main stream and
+    // work-queue heads (kQueueStride apart): one for the main stream and
     // one per overlap slot
     HIPCHK(c, hipMalloc(&c->d_work, kQueueSet * sizeof(unsigned) * (1 + kMaxSlots)));
     int n_cu = 0;
@@ -1799,12 +1760,6 @@ int pt_set_tuning(pt_ctx* c, int key, int value) {
         c->slot = 0;
         return PT_OK;
     }
-    if (key == 10) {
-        if (value < 0 || value > kShards) return fail(c, PT_E_ARG, "queue shards must be 1..8 (0 = automatic)");
-        c->shards = value;
-        drop_graph(c);
-        return PT_OK;
-    }
     if (key == 15) {
         if (value != 0 && value != 1) return fail(c, PT_E_ARG, "culling walk: 0 = automatic, 1 = off");
         c->cons_off = value;
@@ -2062,16 +2017,13 @@ static int enqueue_render(pt_ctx* c, int frame_first, int n_frames, int acc_firs
     // with 128; 4K 3.44 -> 2.64 ms; 4-frame launches 0.83 -> 0.62 ms per frame).  A wave
     // that reserves more ids than it soon needs lengthens the launch tail instead, so longer
     // items and the global-memory scenes' long segments keep 32 (C3 stand-in, one frame per
-    // launch: 3.19 ms with 32, 3.63 with 128).  Tuning key 4 overrides.
+    // launch: 3.19 ms with 32, 3.63 with 128).  With overlapped one-frame launches (2 slots)
+    // 256 ids beat 128 (0.594 vs 0.603 ms per 1080p frame; 64: 0.689).  Tuning key 4 overrides.
     {
         const bool lds_items = lds_staged(c);
         p.pull_batch = c->pull_batch ? c->pull_batch
-                                     : (lds_items && p.group <= 2 ? (p.group == 1 ? 128 : 64) : (int)kPullBatch);
+                                     : (lds_items && p.group <= 2 ? (p.group == 1 ? 256 : 64) : (int)kPullBatch);
     }
-    // queue heads: the short launches' ids are taken fast enough to saturate one device-scope
-    // counter (one 1080p frame per launch), so they spread over kShards heads; long launches
-    // keep one head (their pulls are rare, and one head keeps the global expensive-first order)
-    p.n_shards = c->shards ? c->shards : (n_frames <= kShortLaunch ? kShards : 1);
     {   // exact item / n_groups by ceil(2^32 / n_groups) when item * n_groups < 2^32 for every
         // item (then floor(item * m / 2^32) = floor(item / n_groups)), else the division
         const unsigned long long ng = (unsigned long long)((n_frames + p.group - 1) / p.group);
@@ -2140,21 +2092,18 @@ static int enqueue_render(pt_ctx* c, int frame_first, int n_frames, int acc_firs
         const size_t shade_bytes = (size_t)(3 * c->n_mats + 2 * c->n_spheres) * sizeof(float4);
         p.shade_lds = shade_bytes <= 4096;
         const size_t top_lds = (size_t)p.n_top * 2 * sizeof(float4) + (p.shade_lds ? shade_bytes : 0);
-        // frame-split launches with several queue heads take the SHARD instantiations
-        const bool shard = p.rgb && p.n_shards > 1 && !c->counting;
-#define PT_LAUNCH_SM(L, M, SH)                                                                                \
+#define PT_LAUNCH_SM(L, M)                                                                                \
     if (c->counting && p.rgb) hipLaunchKernelGGL((k_render_sm<true, L, 5, M, true>), grid, dim3(256), L ? lds : top_lds, rs, p); \
     else if (c->counting) hipLaunchKernelGGL((k_render_sm<true, L, 5, M, false>), grid, dim3(256), L ? lds : top_lds, rs, p); \
-    else if (p.rgb && mw == 8 && !M) hipLaunchKernelGGL((k_render_sm<false, L, 8, false, true, false, 256, SH>), grid, dim3(256), L ? lds : top_lds, rs, p); \
-    else if (p.rgb && mw == 7 && !M && L && c->walk_np == kPadNodes) hipLaunchKernelGGL((k_render_sm<false, true, 7, false, true, true, 256, SH>), grid, dim3(256), lds, rs, p); \
-    else if (p.rgb && mw == 7 && !M) hipLaunchKernelGGL((k_render_sm<false, L, 7, false, true, false, 256, SH>), grid, dim3(256), L ? lds : top_lds, rs, p); \
-    else if (p.rgb && mw >= 6) hipLaunchKernelGGL((k_render_sm<false, L, 6, M, true, false, 256, SH>), grid, dim3(256), L ? lds : top_lds, rs, p); \
-    else if (p.rgb) hipLaunchKernelGGL((k_render_sm<false, L, 5, M, true, false, 256, SH>), grid, dim3(256), L ? lds : top_lds, rs, p); \
+    else if (p.rgb && mw == 8 && !M) hipLaunchKernelGGL((k_render_sm<false, L, 8, false, true>), grid, dim3(256), L ? lds : top_lds, rs, p); \
+    else if (p.rgb && mw == 7 && !M && L && c->walk_np == kPadNodes) hipLaunchKernelGGL((k_render_sm<false, true, 7, false, true, true>), grid, dim3(256), lds, rs, p); \
+    else if (p.rgb && mw == 7 && !M) hipLaunchKernelGGL((k_render_sm<false, L, 7, false, true>), grid, dim3(256), L ? lds : top_lds, rs, p); \
+    else if (p.rgb && mw >= 6) hipLaunchKernelGGL((k_render_sm<false, L, 6, M, true>), grid, dim3(256), L ? lds : top_lds, rs, p); \
+    else if (p.rgb) hipLaunchKernelGGL((k_render_sm<false, L, 5, M, true>), grid, dim3(256), L ? lds : top_lds, rs, p); \
     else if (mw >= 6) hipLaunchKernelGGL((k_render_sm<false, L, 6, M, false>), grid, dim3(256), L ? lds : top_lds, rs, p); \
     else hipLaunchKernelGGL((k_render_sm<false, L, 5, M, false>), grid, dim3(256), L ? lds : top_lds, rs, p);
 #define PT_LAUNCH_WIDE(NT, MW)                                                                                \
-    if (shard) hipLaunchKernelGGL((k_render_sm<false, true, MW, false, true, false, NT, true>), grid, dim3(NT), lds, rs, p); \
-    else if (p.rgb) hipLaunchKernelGGL((k_render_sm<false, true, MW, false, true, false, NT>), grid, dim3(NT), lds, rs, p); \
+    if (p.rgb) hipLaunchKernelGGL((k_render_sm<false, true, MW, false, true, false, NT>), grid, dim3(NT), lds, rs, p); \
     else hipLaunchKernelGGL((k_render_sm<false, true, MW, false, false, false, NT>), grid, dim3(NT), lds, rs, p);
         // lds_threads: LDS scene, variant 0, one ray per pixel; the register budget of the
         // waves that are resident (6, 6, 4 per SIMD), not of 7
@@ -2165,10 +2114,10 @@ static int enqueue_render(pt_ctx* c, int frame_first, int n_frames, int acc_firs
 #undef PT_LAUNCH_WIDE
         } else {
             bool multi = p.rpp > 1;
-            if (use_lds && multi) { if (shard) { PT_LAUNCH_SM(true, true, true) } else { PT_LAUNCH_SM(true, true, false) } }
-            else if (use_lds) { if (shard) { PT_LAUNCH_SM(true, false, true) } else { PT_LAUNCH_SM(true, false, false) } }
-            else if (multi) { if (shard) { PT_LAUNCH_SM(false, true, true) } else { PT_LAUNCH_SM(false, true, false) } }
-            else { if (shard) { PT_LAUNCH_SM(false, false, true) } else { PT_LAUNCH_SM(false, false, false) } }
+            if (use_lds && multi) { PT_LAUNCH_SM(true, true) }
+            else if (use_lds) { PT_LAUNCH_SM(true, false) }
+            else if (multi) { PT_LAUNCH_SM(false, true) }
+            else { PT_LAUNCH_SM(false, false) }
 #undef PT_LAUNCH_SM
         }
         if (p.rgb) {

@@ -9,13 +9,15 @@ if [ -n "$AB_TESTS" ]; then
   echo "pytest rc=$rc"; tail -2 "$O/${TAG}_tests.log"
   [ $rc -eq 0 ] || exit $rc
 fi
-timeout -k 10 400 python -u tools/ab_inproc.py --libs ${AB_LIBS:-base,cur} --rounds ${AB_ROUNDS:-5} --spp ${AB_SPP:-1024} --chunk ${AB_SPP:-1024} > "$O/${TAG}_c2.log" 2>&1 || exit $?
-echo "C2:"; grep median "$O/${TAG}_c2.log"
+if [ -n "$AB_LIBS" ]; then
+  timeout -k 10 400 python -u tools/ab_inproc.py --libs $AB_LIBS --rounds ${AB_ROUNDS:-5} --spp ${AB_SPP:-1024} --chunk ${AB_SPP:-1024} > "$O/${TAG}_c2.log" 2>&1 || exit $?
+  echo "C2:"; grep median "$O/${TAG}_c2.log"
+fi
 if [ -n "$AB_C3" ]; then
   timeout -k 10 400 python -u tools/ab_inproc.py --libs ${AB_LIBS:-base,cur} --rounds 3 --scene bunny --spp 64 --chunk 64 > "$O/${TAG}_c3.log" 2>&1 || exit $?
   echo "C3:"; grep median "$O/${TAG}_c3.log"
 fi
 if [ -n "$AB_IFPS" ]; then
-  timeout -k 10 300 python tools/interactive_fps.py --frames 400 --rows none --slots ${IFPS_SLOTS:-0,1} > "$O/${TAG}_ifps.json" 2> "$O/${TAG}_ifps.err" || exit $?
+  timeout -k 10 300 python tools/interactive_fps.py --frames 400 --rows none --combos "${IFPS_COMBOS:-9=0;9=1}" > "$O/${TAG}_ifps.json" 2> "$O/${TAG}_ifps.err" || exit $?
   cat "$O/${TAG}_ifps.json"
 fi

@@ -27,7 +27,9 @@ def main():
     ap.add_argument("--bounces", type=int, default=8)
     ap.add_argument("--scene", default="cornell")
     ap.add_argument("--rows", default="none,rgba8_aces,rgba32f")
-    ap.add_argument("--slots", default="0,1", help="tuning key 9 values: 0 = automatic, 1 = no overlap, 2..4")
+    ap.add_argument("--combos", default="9=0;9=1",
+                    help="tuning settings to run, ';'-separated, each a ','-list of key=value (pt_set_tuning); "
+                         "row suffix: '' for 9=0 (automatic overlap), '_no_overlap' for 9=1, else the settings")
     a = ap.parse_args()
     sb = H.setupBuffers(*pt_scenes.write_scene(a.scene, os.path.join(REPO, "scenes")))
     pt = H.PathTracer(a.width, a.height, max_bounce=a.bounces)
@@ -41,9 +43,15 @@ def main():
     pt.set_counting(False)
     out = {"width": a.width, "height": a.height, "bounces": a.bounces, "scene": a.scene, "frames": a.frames,
            "scene_upload_ms": round(upload_s * 1e3, 3), "segments_per_frame": seg_per_frame}
-    for slots in (int(x) for x in a.slots.split(",")):
-        pt.set_key(9, slots)
-        suffix = "" if slots == 0 else ("_no_overlap" if slots == 1 else "_slots%d" % slots)
+    touched = set()
+    for combo in a.combos.split(";"):
+        kv = [tuple(int(x) for x in item.split("=")) for item in combo.split(",") if item]
+        for k in touched:                                     # back to automatic
+            pt.set_key(k, 0)
+        for k, v in kv:
+            pt.set_key(k, v)
+            touched.add(k)
+        suffix = {"9=0": "", "9=1": "_no_overlap"}.get(combo, "_" + combo.replace("=", "_").replace(",", "_"))
         for readback in a.rows.split(","):
             v = H.Viewer()
             for i in range(70):                               # warm-up (and the first tile sorts)
@@ -59,7 +67,10 @@ def main():
             pt.sync()
             dt = time.perf_counter() - t0
             v.close()
-            out[readback + suffix] = {
+            name = readback + suffix
+            while name in out:                                # a repeated setting: keep every row
+                name += "+"
+            out[name] = {
                 "ms_per_frame": round(dt * 1e3 / a.frames, 4), "fps": round(a.frames / dt, 1),
                 "mrays_per_s": round(seg_per_frame * a.frames / dt / 1e6, 1)}
     pt.close()
