@@ -132,6 +132,10 @@ def lib():
             "pt_viewer_frame": (ip, [vp, vp, C.c_double, C.POINTER(ViewerFrame)]),
         }
         for name, (res, args) in sig.items():
+            # tools/ab_inproc.py loads older builds beside this one: PT_LIB_PARTIAL=1 lets a
+            # build without the newer entry points load (the product always binds all of them)
+            if os.environ.get("PT_LIB_PARTIAL") == "1" and not hasattr(L, name):
+                continue
             fn = getattr(L, name)
             fn.restype = res
             fn.argtypes = args

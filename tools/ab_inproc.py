@@ -21,10 +21,12 @@ import pt_scenes  # noqa: E402
 def load_host(name):
     path = os.path.join(PKG, "build", "libptrace.so" if name == "cur" else "libptrace_%s.so" % name)
     os.environ["PT_LIB"] = path
+    os.environ["PT_LIB_PARTIAL"] = "1" if name != "cur" else "0"
     spec = importlib.util.spec_from_file_location("pt_host_" + name, os.path.join(PKG, "pt_host.py"))
     mod = importlib.util.module_from_spec(spec)
     spec.loader.exec_module(mod)
     assert mod.LIB_PATH == path
+    mod.lib()   # bind now, while PT_LIB_PARTIAL describes this build
     return mod
 
 
@@ -38,6 +40,8 @@ def main():
     ap.add_argument("--tris", type=int, default=0, help="generator target_tris (bunny / sponza)")
     ap.add_argument("--width", type=int, default=1920)
     ap.add_argument("--height", type=int, default=1080)
+    ap.add_argument("--world", type=int, default=1, help="render rank 0 of a WORLD-way row split (per-GPU share)")
+    ap.add_argument("--key", action="append", default=[], help="pt_set_tuning key=value for every build (repeatable)")
     a = ap.parse_args()
     libs = a.libs.split(",")
     hosts = {l: load_host(l) for l in libs}
@@ -47,8 +51,11 @@ def main():
     pts, seg = {}, {}
     for l in libs:
         H = hosts[l]
-        pt = H.PathTracer(a.width, a.height, max_bounce=8)
+        pt = H.PathTracer(a.width, a.height, max_bounce=8, rank=0, world=a.world)
         pt.upload(H.setupBuffers(obj, mtl))
+        for kv in a.key:
+            k, v = (int(x) for x in kv.split("="))
+            pt.set_key(k, v)
         pt.set_counting(True)
         total = 0
         for f0 in range(1, a.spp + 1, a.chunk):

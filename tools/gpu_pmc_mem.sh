@@ -1,7 +1,7 @@
 #!/bin/bash
 # PMC passes on the vector-memory pipeline (TA / TD / TCP, UTCL1) for a global-memory scene
 # (default the C3 stand-in), each counter group in its own rocprofv3 run.
-cd "$GRAFT_REPO_ROOT"; R="$GRAFT_REPO_ROOT"; OUT="$R/gpurun_out/pmcm"; mkdir -p "$OUT"
+cd "$GRAFT_REPO_ROOT"; R="$GRAFT_REPO_ROOT"; OUT="$R/gpurun_out/${PMCM_DIR:-pmcm}"; mkdir -p "$OUT"
 export TMPDIR=/tmp
 cd /tmp
 ARGS=${PMC_ARGS:-"--scene bunny --chunk 64 --launches 1"}

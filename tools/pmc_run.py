@@ -18,10 +18,14 @@ ap.add_argument("--variant", type=int, default=0)
 ap.add_argument("--scene", default="cornell")
 ap.add_argument("--width", type=int, default=1920)
 ap.add_argument("--height", type=int, default=1080)
+ap.add_argument("--key", action="append", default=[], help="pt_set_tuning key=value (repeatable)")
 a = ap.parse_args()
 sb = pt_host.setupBuffers(*pt_scenes.write_scene(a.scene, os.path.join(REPO, "scenes")))
 pt = pt_host.PathTracer(a.width, a.height, max_bounce=8)
 pt.set_kernel(a.variant)
+for kv in a.key:
+    k, v = (int(x) for x in kv.split("="))
+    pt.set_key(k, v)
 pt.upload(sb)
 # the bench's step: frames 1..chunk from accumulate = 0, re-rendered (warm-up launch first)
 for i in range(a.launches + 1):
