@@ -1793,6 +1793,9 @@ int pt_set_tuning(pt_ctx* c, int key, int value) {
         c->minw = value;
     }
     else if (key == 2) {
+        // a learned order stays when the setting does not change (re-applying the default must
+        // not send the next long render back through the cold probe launch)
+        if ((value != 0) == c->adaptive) return PT_OK;
         c->adaptive = value != 0;
         c->order_sorted = false;
         c->order_skip = 0;
