@@ -5,9 +5,9 @@
 //     correctly rounded division and square root;
 //   * dot(a,b) = (a.x*b.x + a.y*b.y) + a.z*b.z ; cross per the GLSL spec;
 //   * normalize(v) = v * (1 / sqrt(dot(v,v))) ; mix(x,y,a) = x*(1-a) + y*a ;
-//   * log: fdlibm e_logf algorithm; cos: Cephes cosf algorithm (octant reduction, 3-part pi/4).
+//   * log / cos: the build's pinned polynomials (logf_pinned, cosf_pinned below).
 // computeShader.c leaves transcendental precision to the GL driver (implementation-defined);
-// these are the build's pinned choices (both < 2 ulp on the ranges the hot path feeds).
+// these are the build's pinned choices.
 #pragma once
 
 #include <stdint.h>
@@ -27,14 +27,14 @@ PT_HD uint32_t fbits(float f) {
 #if defined(__HIP_DEVICE_COMPILE__)
     return __float_as_uint(f);
 #else
-    uint32_t u; memcpy(&u, &f, 4); return u;
+    uint32_t u; __builtin_memcpy(&u, &f, 4); return u;
 #endif
 }
 PT_HD float bitsf(uint32_t u) {
 #if defined(__HIP_DEVICE_COMPILE__)
     return __uint_as_float(u);
 #else
-    float f; memcpy(&f, &u, 4); return f;
+    float f; __builtin_memcpy(&f, &u, 4); return f;
 #endif
 }
 PT_HD float fsqrt(float x) {
@@ -81,155 +81,51 @@ PT_HD float div_mk(float a, float b, float rb) {
     return __builtin_fmaf(r, rb, q);
 }
 
-// fdlibm e_logf (FreeBSD constants).  x in {0} U [2^-32, 1] on the hot path.
+// log and cos of the Box-Muller draw (computeShader.c:115-120).  GLSL leaves their precision
+// to the driver (GLSL 4.30 §4.7.1: log within 3 ulp, cos within 2^-11 absolute), and the
+// reference's image depends on the driver's choice; these are the build's pinned choices,
+// restated independently by the oracle (oracle/pt_oracle.cpp) and its numpy twin.  Both are
+// branch-free polynomials in fma (exactly rounded on the CPU's FMA and on v_fma_f32, so host
+// and device agree bit for bit: tools/verify_fastmath.hip, tests/test_exact_div.py).
+// Measured over every binary32 of the hot-path domains (tests/test_oracle_pinning.py):
+//   logf_pinned: at most 1.2 ulp;  cosf_pinned: at most 1.06e-7 absolute.
+// (Rounds 1-2 pinned fdlibm e_logf and Cephes cosf: 58 and 41 VALU against 22 and 18 here,
+// +5.7% on C2.)
+//
+// log(x), x in {0} U [2^-32, 1]: x = 2^k z with z in [0.699, 1.398) (the exponent split at
+// 0x3f330000), f = z - 1, log(1 + f) = f + f^2 P(f) with P a degree-7 fit (relative error
+// 3e-8 on the interval), then + k ln2 in two parts (k * ln2_hi exact).  log(0) = -inf.
 PT_HD float logf_pinned(float x) {
-    const float ln2_hi = 6.9313812256e-01f, ln2_lo = 9.0580006145e-06f, two25 = 3.355443200e+07f;
-    const float Lg1 = bitsf(0x3f2aaaaau), Lg2 = bitsf(0x3ecccce1u), Lg3 = bitsf(0x3e91e9eeu),
-                Lg4 = bitsf(0x3e789e26u);
-    int32_t ix = (int32_t)fbits(x);
-    int32_t k = 0;
-    if (ix < 0x00800000) {
-        if ((ix & 0x7fffffff) == 0) return bitsf(0xff800000u);   // -inf
-        if (ix < 0) return bitsf(0x7fc00000u);                    // NaN
-        k -= 25; x *= two25; ix = (int32_t)fbits(x);
-    }
-    if (ix >= 0x7f800000) return x + x;
-    k += (ix >> 23) - 127;
-    ix &= 0x007fffff;
-    int32_t i = (ix + (0x95f64 << 3)) & 0x800000;
-    x = bitsf((uint32_t)(ix | (i ^ 0x3f800000)));
-    k += (i >> 23);
-    float f = x - 1.0f;
-    float dk;
-    if ((0x007fffff & (0x8000 + ix)) < 0xc000) {
-        if (f == 0.0f) {
-            if (k == 0) return 0.0f;
-            dk = (float)k;
-            return dk * ln2_hi + dk * ln2_lo;
-        }
-        float R = f * f * (0.5f - 0.33333333333333333f * f);
-        if (k == 0) return f - R;
-        dk = (float)k;
-        return dk * ln2_hi - ((R - dk * ln2_lo) - f);
-    }
-    // |f| >= 2^-20 on this path (the branch above takes smaller f) and 2+f in [1.58, 2.42]:
-    // the quotient by an exact reciprocal (rcp_fast) and a Markstein correction
-    const float tf = 2.0f + f;
-    float s = div_mk(f, tf, rcp_fast(tf));
-    dk = (float)k;
-    float z = s * s;
-    int32_t ii = ix - (0x6147a << 3);
-    float w = z * z;
-    int32_t j = (0x6b851 << 3) - ix;
-    float t1 = w * (Lg2 + w * Lg4);
-    float t2 = z * (Lg1 + w * Lg3);
-    ii |= j;
-    float R = t2 + t1;
-    if (ii > 0) {
-        float hfsq = 0.5f * f * f;
-        if (k == 0) return f - (hfsq - s * (hfsq + R));
-        return dk * ln2_hi - ((hfsq - (s * (hfsq + R) + dk * ln2_lo)) - f);
-    }
-    if (k == 0) return f - s * (f - R);
-    return dk * ln2_hi - ((s * (f - R) - dk * ln2_lo) - f);
-}
-
-// Cephes cosf; valid for finite |x| < 8192 (the hot path feeds [0, 2*pi]).
-PT_HD float cosf_pinned(float xx) {
-    uint32_t ax = fbits(xx) & 0x7fffffffu;
-    if (ax >= 0x7f800000u) return bitsf(0x7fc00000u);
-    const float DP1 = 0.78515625f, DP2 = 2.4187564849853515625e-4f, DP3 = 3.77489497744594108e-8f,
-                FOPI = 1.27323954473516f;
-    float x = bitsf(ax);
-    int j = (int)(FOPI * x);
-    float y = (float)j;
-    if (j & 1) { j += 1; y += 1.0f; }
-    j &= 7;
-    bool neg = false;
-    if (j > 3) { j -= 4; neg = !neg; }
-    if (j > 1) neg = !neg;
-    x = ((x - y * DP1) - y * DP2) - y * DP3;
-    float z = x * x;
-    float r;
-    if (j == 1 || j == 2) {
-        r = ((-1.9515295891E-4f * z + 8.3321608736E-3f) * z - 1.6666654611E-1f) * z * x + x;
-    } else {
-        r = ((2.443315711809948E-005f * z - 1.388731625493765E-003f) * z + 4.166664568298827E-002f) * z * z;
-        r -= 0.5f * z;
-        r += 1.0f;
-    }
-    return neg ? -r : r;
-}
-
-// Branch-free forms of logf_pinned / cosf_pinned for the kernels' Box-Muller draw: the same
-// operations on the same values, every fdlibm / Cephes branch evaluated and chosen by a
-// select (a wave otherwise runs each divergent branch in turn, with exec-mask bookkeeping).
-// Bit-identical to the branchy forms over their whole hot-path domains (x in {0} U
-// [2^-32, 1] for log, every finite theta in [0, 2*pi] for cos): checked exhaustively on the
-// host (tests/test_exact_div.py) and on the GPU (tools/verify_fastmath.hip).
-//   log: fdlibm's k == 0 returns are the general k != 0 expressions with dk = +0 (RN(a - b)
-//   = -RN(b - a), x - 0 = x, and 0 - (+-0) = +0 = f - f), so only the small-|f| / main and
-//   ii > 0 choices remain; f == 0 (x a power of two) is the small-|f| expression at f = 0.
-PT_HD float logf_bf(float x) {                     // x in {0} U [2^-32, 1]
-    const float ln2_hi = 6.9313812256e-01f, ln2_lo = 9.0580006145e-06f;
-    const float Lg1 = bitsf(0x3f2aaaaau), Lg2 = bitsf(0x3ecccce1u), Lg3 = bitsf(0x3e91e9eeu),
-                Lg4 = bitsf(0x3e789e26u);
-    int32_t ix = (int32_t)fbits(x);
-    int32_t k = (ix >> 23) - 127;
-    ix &= 0x007fffff;
-    const int32_t i = (ix + (0x95f64 << 3)) & 0x800000;
-    const float xr = bitsf((uint32_t)(ix | (i ^ 0x3f800000)));
-    k += (i >> 23);
-    const float f = xr - 1.0f;
-    const float dk = (float)k;
-    const float hi = dk * ln2_hi, lo = dk * ln2_lo;
-    // main branch (2 + f in [1.58, 2.42]: exact reciprocal + Markstein, as logf_pinned)
-    const float tf = 2.0f + f;
-    const float s = div_mk(f, tf, rcp_fast(tf));
-    const float z = s * s;
-    const float w = z * z;
-    const float t1 = w * (Lg2 + w * Lg4);
-    const float t2 = z * (Lg1 + w * Lg3);
-    const float R = t2 + t1;
-    const int32_t ii = (ix - (0x6147a << 3)) | ((0x6b851 << 3) - ix);
-    const float hfsq = 0.5f * f * f;
-    const float m1 = hi - ((hfsq - (s * (hfsq + R) + lo)) - f);
-    const float m2 = hi - ((s * (f - R) - lo) - f);
-    float r = ii > 0 ? m1 : m2;
-    // |f| < 2^-20 branch (x within ~2^-20 of a power of two: about 1 draw in 2^19), run
-    // only when a lane of the wave needs it
-    const bool is_small = (0x007fffff & (0x8000 + ix)) < 0xc000;
-#if defined(__HIP_DEVICE_COMPILE__)
-    if (__any(is_small))
-#endif
-    {
-        const float Rs = f * f * (0.5f - 0.33333333333333333f * f);
-        const float small = hi - ((Rs - lo) - f);
-        r = is_small ? small : r;
-    }
+    const uint32_t ix = fbits(x);
+    const uint32_t tmp = ix - 0x3f330000u;
+    const int k = (int32_t)tmp >> 23;
+    const float z = bitsf(ix - (tmp & 0xff800000u));
+    const float f = z - 1.0f, f2 = f * f;
+    float P = __builtin_fmaf(f, 0x1.87c9c0p-4f, -0x1.2bf636p-3f);
+    P = __builtin_fmaf(f, P, 0x1.2f3194p-3f);
+    P = __builtin_fmaf(f, P, -0x1.52694ep-3f);
+    P = __builtin_fmaf(f, P, 0x1.98eb62p-3f);
+    P = __builtin_fmaf(f, P, -0x1.000924p-2f);
+    P = __builtin_fmaf(f, P, 0x1.5556ccp-2f);
+    P = __builtin_fmaf(f, P, -0x1.fffff0p-2f);
+    const float kf = (float)k;
+    const float r = __builtin_fmaf(kf, 0x1.62e300p-1f, __builtin_fmaf(kf, 0x1.2fefa2p-17f, __builtin_fmaf(f2, P, f)));
     return x == 0.0f ? bitsf(0xff800000u) : r;
 }
-PT_HD float cosf_bf(float xx) {                    // finite xx >= 0 (theta in [0, 2*pi])
-    const float DP1 = 0.78515625f, DP2 = 2.4187564849853515625e-4f, DP3 = 3.77489497744594108e-8f,
-                FOPI = 1.27323954473516f;
-    const float x0 = bitsf(fbits(xx) & 0x7fffffffu);
-    int j = (int)(FOPI * x0);
-    float y = (float)j;
-    const bool odd = (j & 1) != 0;
-    j = odd ? j + 1 : j;
-    y = odd ? y + 1.0f : y;
-    j &= 7;
-    bool neg = j > 3;
-    j = j > 3 ? j - 4 : j;
-    neg = (j > 1) != neg;
-    const float x = ((x0 - y * DP1) - y * DP2) - y * DP3;
-    const float z = x * x;
-    const float rs = ((-1.9515295891E-4f * z + 8.3321608736E-3f) * z - 1.6666654611E-1f) * z * x + x;
-    float rc = ((2.443315711809948E-005f * z - 1.388731625493765E-003f) * z + 4.166664568298827E-002f) * z * z;
-    rc -= 0.5f * z;
-    rc += 1.0f;
-    const float r = (j == 1 || j == 2) ? rs : rc;
-    return neg ? -r : r;
+// cos(t), t in [0, 2 pi] (the draw's angle): q = rint(t 2/pi), r = t - q pi/2 (two-part
+// pi/2 by fma, |r| <= pi/4), then cos r or sin r by degree-6 / degree-7 fits (absolute error
+// 3e-8 / 2e-9) for quadrant q mod 4, negated in quadrants 1 and 2.
+PT_HD float cosf_pinned(float t) {
+    const float qf = __builtin_rintf(t * 0x1.45f306p-1f);
+    float r = __builtin_fmaf(-qf, 0x1.921fb6p+0f, t);
+    r = __builtin_fmaf(-qf, -0x1.777a5cp-25f, r);
+    const float r2 = r * r;
+    const float c = __builtin_fmaf(r2, __builtin_fmaf(r2, __builtin_fmaf(r2, -0x1.64756cp-10f, 0x1.553f94p-5f), -0x1.ffffbap-2f), 1.0f);
+    const float u = __builtin_fmaf(r2, __builtin_fmaf(r2, -0x1.98da64p-13f, 0x1.1105b4p-7f), -0x1.555540p-3f);
+    const float sn = __builtin_fmaf(r * r2, u, r);
+    const int q = (int)qf;
+    const float v = (q & 1) ? sn : c;
+    return bitsf(fbits(v) ^ ((uint32_t)((q + 1) & 2) << 30));
 }
 
 struct f3 { float x, y, z; };
@@ -291,13 +187,8 @@ PT_HD float random_normal(uint32_t& s) {            // :115-120 (theta first, th
     // or 0: no subnormal) and so is the constant's 2^-32 scaling, so both forms round the same
     // real product
     float theta = (float)next_random(s) * ((2.0f * 3.1415926f) * (1.0f / 4294967296.0f));
-#if defined(__HIP_DEVICE_COMPILE__)
-    float rho = sqrt_g(-2.0f * logf_bf(random01(s)));
-    return rho * cosf_bf(theta);
-#else
     float rho = sqrt_g(-2.0f * logf_pinned(random01(s)));
     return rho * cosf_pinned(theta);
-#endif
 }
 PT_HD f3 random_unit_vector(uint32_t& s) {          // :122-129, x, y, z order
     float x = random_normal(s);

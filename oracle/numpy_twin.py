@@ -7,9 +7,9 @@ code with oracle/pt_oracle.cpp; tests require the two to agree bit for bit, whic
 C++ oracle against transcription slips.  Small images only (pure numpy, masked loops).
 
 Arithmetic: numpy binary32 array ops are IEEE round-to-nearest (no FMA), np.sqrt and '/'
-are correctly rounded -- the same pinning as DESIGN.md §3.2.  log/cos follow the same
-published algorithms (fdlibm e_logf, Cephes cosf) re-implemented here with int32/float32
-array arithmetic.
+are correctly rounded -- the same pinning as DESIGN.md §3.2.  log/cos are the build's pinned
+polynomials, re-implemented here with uint32/float32 array arithmetic and an exactly rounded
+binary32 fma emulation (numpy has no fma).
 """
 from __future__ import annotations
 
@@ -29,88 +29,66 @@ def _float(b):
 
 
 # ------------------------------------------------------------------ transcendentals
+def fma(a, b, c):
+    """Correctly rounded binary32 fused multiply-add, vectorised: a*b is exact in binary64,
+    TwoSum gives the exact a*b + c as s + e, and the binary64 -> binary32 rounding of s is
+    corrected when s sits exactly on a binary32 rounding midpoint (the only case where the
+    double rounding can differ: midpoints are binary64 numbers, so RN64 never crosses one)."""
+    a, b, c = (np.asarray(v, f32).astype(np.float64) for v in (a, b, c))
+    p = a * b
+    s = p + c
+    bb = s - p
+    e = (p - (s - bb)) + (c - bb)
+    r = s.astype(f32)
+    rr = r.astype(np.float64)
+    d = s - rr
+    nb = np.nextafter(r, np.where(d > 0, f32(np.inf), f32(-np.inf)).astype(f32))
+    mid = (d != 0) & (np.abs(nb.astype(np.float64) - rr) == 2 * np.abs(d))
+    fix = mid & (e != 0) & (np.sign(e) == np.sign(d))
+    return np.where(fix, nb, r).astype(f32)
+
+
+_LOGP = [float.fromhex(h) for h in ("0x1.87c9c0p-4", "-0x1.2bf636p-3", "0x1.2f3194p-3", "-0x1.52694ep-3",
+                                     "0x1.98eb62p-3", "-0x1.000924p-2", "0x1.5556ccp-2", "-0x1.fffff0p-2")]
+
+
 def logf(x):
-    x = np.array(x, f32, copy=True)
-    ix = _bits(x).copy()
-    k = np.zeros_like(ix)
-    out = np.full(x.shape, np.nan, f32)
-    done = np.zeros(x.shape, bool)
-    zero = (ix & 0x7FFFFFFF) == 0
-    out[zero] = -np.inf
-    done |= zero
-    neg = (ix < 0) & ~done
-    out[neg] = np.nan
-    done |= neg
-    sub = (ix < 0x00800000) & ~done
-    if sub.any():
-        k[sub] -= 25
-        x[sub] = x[sub] * f32(3.355443200e+07)
-        ix[sub] = _bits(x[sub])
-    special = (ix >= 0x7F800000) & ~done
-    out[special] = x[special] + x[special]
-    done |= special
-    k = k + ((ix >> 23) - 127)
-    ix = ix & 0x007FFFFF
-    i = (ix + (0x95F64 << 3)) & 0x800000
-    xn = _float(ix | (i ^ 0x3F800000))
-    k = k + (i >> 23)
-    f = xn - f32(1.0)
-    ln2_hi, ln2_lo = f32(6.9313812256e-01), f32(9.0580006145e-06)
-    dk = k.astype(f32)
-    small = ((0x007FFFFF & (0x8000 + ix)) < 0xC000) & ~done
-    # small |f| branch
-    fz = small & (f == 0)
-    out[fz & (k == 0)] = f32(0.0)
-    m = fz & (k != 0)
-    out[m] = dk[m] * ln2_hi + dk[m] * ln2_lo
-    m = small & (f != 0)
-    R = f * f * (f32(0.5) - f32(0.33333333333333333) * f)
-    mm = m & (k == 0)
-    out[mm] = (f - R)[mm]
-    mm = m & (k != 0)
-    out[mm] = (dk * ln2_hi - ((R - dk * ln2_lo) - f))[mm]
-    big = ~small & ~done
-    s = f / (f32(2.0) + f)
-    z = s * s
-    ii = ix - (0x6147A << 3)
-    w = z * z
-    j = (0x6B851 << 3) - ix
-    Lg1, Lg2, Lg3, Lg4 = (_float(np.int32(v)) for v in (0x3F2AAAAA, 0x3ECCCCE1, 0x3E91E9EE, 0x3E789E26))
-    t1 = w * (Lg2 + w * Lg4)
-    t2 = z * (Lg1 + w * Lg3)
-    ii = ii | j
-    R = t2 + t1
-    hfsq = f32(0.5) * f * f
-    a = big & (ii > 0)
-    out[a & (k == 0)] = (f - (hfsq - s * (hfsq + R)))[a & (k == 0)]
-    out[a & (k != 0)] = (dk * ln2_hi - ((hfsq - (s * (hfsq + R) + dk * ln2_lo)) - f))[a & (k != 0)]
-    b = big & ~(ii > 0)
-    out[b & (k == 0)] = (f - s * (f - R))[b & (k == 0)]
-    out[b & (k != 0)] = (dk * ln2_hi - ((s * (f - R) - dk * ln2_lo) - f))[b & (k != 0)]
-    return out
+    """The build's pinned log (pt_math.h logf_pinned), for x in {0} U [2^-32, 1]:
+    x = 2^k z split at the exponent boundary 0x3f330000, f = z - 1, f + f^2 P(f) by Horner in
+    fma, then + k ln2_lo and + k ln2_hi."""
+    x = np.asarray(x, f32)
+    ix = x.view(u32)
+    split = (ix - u32(0x3F330000)).astype(u32)
+    k = split.view(i32) >> 23
+    z = (ix - (split & u32(0xFF800000))).astype(u32).view(f32)
+    f = z - f32(1.0)
+    P = np.full(x.shape, f32(_LOGP[0]), f32)
+    for c in _LOGP[1:]:
+        P = fma(f, P, f32(c))
+    kf = k.astype(f32)
+    y = fma(f * f, P, f)
+    y = fma(kf, f32(float.fromhex("0x1.2fefa2p-17")), y)
+    y = fma(kf, f32(float.fromhex("0x1.62e300p-1")), y)
+    return np.where(x == 0, f32(-np.inf), y).astype(f32)
 
 
-def cosf(xx):
-    xx = np.asarray(xx, f32)
-    x = np.abs(xx)
-    j = (f32(1.27323954473516) * x).astype(np.int64).astype(i32)
-    y = j.astype(f32)
-    odd = (j & 1) == 1
-    j = np.where(odd, j + 1, j)
-    y = np.where(odd, y + f32(1.0), y)
-    j = j & 7
-    neg = j > 3
-    j = np.where(neg, j - 4, j)
-    neg = np.where(j > 1, ~neg, neg)
-    x = ((x - y * f32(0.78515625)) - y * f32(2.4187564849853515625e-4)) - y * f32(3.77489497744594108e-8)
-    z = x * x
-    s = ((f32(-1.9515295891E-4) * z + f32(8.3321608736E-3)) * z - f32(1.6666654611E-1)) * z * x + x
-    c = ((f32(2.443315711809948E-005) * z - f32(1.388731625493765E-003)) * z + f32(4.166664568298827E-002)) * z * z
-    c = c - f32(0.5) * z
-    c = c + f32(1.0)
-    r = np.where((j == 1) | (j == 2), s, c)
-    r = np.where(neg, -r, r)
-    return np.where(np.isfinite(xx), r, f32(np.nan)).astype(f32)
+def cosf(t):
+    """The build's pinned cos (pt_math.h cosf_pinned) for t in [0, 2 pi]: quadrant q =
+    rint(t 2/pi), r = t - q pi/2 (two-part pi/2 by fma), cos r or sin r polynomial."""
+    t = np.asarray(t, f32)
+    q = np.rint(t * f32(float.fromhex("0x1.45f306p-1"))).astype(f32)
+    r = fma(-q, f32(float.fromhex("0x1.921fb6p+0")), t)
+    r = fma(-q, f32(float.fromhex("-0x1.777a5cp-25")), r)
+    r2 = r * r
+    cp = fma(r2, f32(float.fromhex("-0x1.64756cp-10")), f32(float.fromhex("0x1.553f94p-5")))
+    cp = fma(r2, cp, f32(float.fromhex("-0x1.ffffbap-2")))
+    c = fma(r2, cp, f32(1.0))
+    sp = fma(r2, f32(float.fromhex("-0x1.98da64p-13")), f32(float.fromhex("0x1.1105b4p-7")))
+    sp = fma(r2, sp, f32(float.fromhex("-0x1.555540p-3")))
+    sn = fma(r * r2, sp, r)
+    quad = q.astype(i32) & 3
+    v = np.where((quad & 1) == 1, sn, c)
+    return np.where((quad == 1) | (quad == 2), -v, v).astype(f32)
 
 
 # ------------------------------------------------------------------ RNG

