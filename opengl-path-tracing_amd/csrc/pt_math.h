@@ -110,7 +110,9 @@ PT_HD float logf_pinned(float x) {
     P = __builtin_fmaf(f, P, -0x1.fffff0p-2f);
     const float kf = (float)k;
     const float r = __builtin_fmaf(kf, 0x1.62e300p-1f, __builtin_fmaf(kf, 0x1.2fefa2p-17f, __builtin_fmaf(f2, P, f)));
-    return x == 0.0f ? bitsf(0xff800000u) : r;
+    // log 0 = -inf by a select on the bits (x = +0 has no other encoding here): a compare on
+    // the float made the compiler branch around the whole polynomial
+    return ix == 0u ? bitsf(0xff800000u) : r;
 }
 // cos(t), t in [0, 2 pi] (the draw's angle): q = rint(t 2/pi), r = t - q pi/2 (two-part
 // pi/2 by fma, |r| <= pi/4), then cos r or sin r by degree-6 / degree-7 fits (absolute error
@@ -187,7 +189,10 @@ PT_HD float random_normal(uint32_t& s) {            // :115-120 (theta first, th
     // or 0: no subnormal) and so is the constant's 2^-32 scaling, so both forms round the same
     // real product
     float theta = (float)next_random(s) * ((2.0f * 3.1415926f) * (1.0f / 4294967296.0f));
-    float rho = sqrt_g(-2.0f * logf_pinned(random01(s)));
+    // -2 log(u) is 0 (u = 1), +inf (u = 0) or in [2^-24, 45]: inside sqrt_fast's guard except
+    // the two ends, which are their own roots -- a select instead of sqrt_g's branch
+    const float q = -2.0f * logf_pinned(random01(s));
+    const float rho = ((q == 0.0f) | (q == __builtin_huge_valf())) ? q : sqrt_fast(q);
     return rho * cosf_pinned(theta);
 }
 PT_HD f3 random_unit_vector(uint32_t& s) {          // :122-129, x, y, z order
