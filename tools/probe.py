@@ -45,6 +45,7 @@ def main():
     ap.add_argument("--tunings", default="0:0", help="leaf:shade[:adaptive[:waves[:group[:floor[:compact]]]]] for variants 0/3, comma list")
     ap.add_argument("--world", type=int, default=1, help="render rank 0 of a WORLD-way row split (per-GPU share)")
     ap.add_argument("--flags", type=int, default=0, help="PT_FLAG_* bits (32 = Moller-Trumbore mode)")
+    ap.add_argument("--key", action="append", default=[], help="pt_set_tuning key=value after each tuning (repeatable)")
     a = ap.parse_args()
     sb = pt_host.setupBuffers(*pt_scenes.write_scene(a.scene, os.path.join(REPO, "scenes")))
     pt = pt_host.PathTracer(a.width, a.height, max_bounce=a.bounces, rank=0, world=a.world, flags=a.flags)
@@ -59,6 +60,9 @@ def main():
             pt.set_tuning(parts[0], parts[1], parts[2] if len(parts) > 2 else 1,
                           parts[3] if len(parts) > 3 else 0, parts[4] if len(parts) > 4 else None,
                           parts[5] if len(parts) > 5 else None, parts[6] if len(parts) > 6 else None)
+        for kv in a.key:
+            k, val = (int(x) for x in kv.split("="))
+            pt.set_key(k, val)
 
     for v, c, tu in configs:
         apply(v, tu)
