@@ -192,3 +192,32 @@ def test_overlapped_reset_and_camera_change(cornell_scene):
     got = pt.read_rgba32f()
     pt.close()
     assert_bitwise(got, want, "reset after camera move")
+
+
+@pytest.mark.parametrize("slots", [2, 3, 4])
+def test_overlap_slots_grow_and_switch(cornell_scene, slots):
+    """Overlap slots whose colour scratch must grow while earlier renders are in flight
+    (launches of 1, then 16, then 1 frames rotate over the slots: ensure_slot drains the slot's
+    stream and the accumulate stream before reallocating), a counting render in between (never
+    overlapped), and the slot count switched mid-sequence: the oracle's image."""
+    W, Hh = 56, 36
+    want, cnt = O.render(cornell_scene, W, Hh, max_bounce=6, n_frames=70, counters=True)
+    pt = H.PathTracer(W, Hh, max_bounce=6)
+    pt.set_key(9, slots)
+    pt.upload(cornell_scene)
+    f = 1
+    for n in [1, 1, 16, 1, 16, 1, 1, 16]:           # frames 1..53
+        pt.render_async(f, n, 0 if f == 1 else 1)
+        f += n
+    pt.set_counting(True)
+    pt.render(f, 3, 1)                              # 54..56, counted, on the context stream
+    pt.set_counting(False)
+    f += 3
+    pt.set_key(9, 2 if slots != 2 else 4)
+    for n in [1, 2, 1, 4, 1, 5]:                    # 57..70
+        pt.render_async(f, n, 1)
+        f += n
+    got = pt.read_rgba32f()
+    pt.close()
+    assert f == 71
+    assert_bitwise(got, want, "%d slots" % slots)
