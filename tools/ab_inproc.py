@@ -3,7 +3,8 @@ ctypes handle through its own copy of pt_host), and their renders are interleave
 round, so clock and thermal drift between processes does not enter the comparison.
 
 python tools/ab_inproc.py --libs base,cur --rounds 4 --spp 128 --chunk 128 [--scene bunny [--tris 300]]
-('cur' = build/libptrace.so, other names = build/libptrace_<name>.so from tools/ab_build.sh)
+('cur' = build/libptrace.so, other names = build/libptrace_<name>.so from tools/ab_build.sh;
+ an entry name:k=v[:k=v] adds pt_set_tuning keys for that entry only, e.g. --libs cur,p37:3=8)
 """
 import argparse
 import importlib.util
@@ -44,7 +45,13 @@ def main():
     ap.add_argument("--key", action="append", default=[], help="pt_set_tuning key=value for every build (repeatable)")
     a = ap.parse_args()
     libs = a.libs.split(",")
-    hosts = {l: load_host(l) for l in libs}
+    mods = {}
+    for l in libs:
+        name = l.split(":")[0]
+        if name not in mods:
+            mods[name] = load_host(name)
+    hosts = {l: mods[l.split(":")[0]] for l in libs}
+    own_keys = {l: l.split(":")[1:] for l in libs}
     kw = {"target_tris": a.tris} if a.tris else {}
     obj, mtl = pt_scenes.write_scene(a.scene, os.path.join(REPO, "scenes", "%s_%d" % (a.scene, a.tris)) if a.tris
                                      else os.path.join(REPO, "scenes"), **kw)
@@ -53,7 +60,7 @@ def main():
         H = hosts[l]
         pt = H.PathTracer(a.width, a.height, max_bounce=8, rank=0, world=a.world)
         pt.upload(H.setupBuffers(obj, mtl))
-        for kv in a.key:
+        for kv in a.key + own_keys[l]:
             k, v = (int(x) for x in kv.split("="))
             pt.set_key(k, v)
         pt.set_counting(True)
