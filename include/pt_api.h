@@ -101,6 +101,18 @@ int pt_get_config(const pt_ctx* ctx, pt_config* out);
 int pt_read_rgba32f(pt_ctx* ctx, float* host_dst, size_t bytes);
 /* ACES-tonemapped RGBA8 of the local rows, computed on the device. */
 int pt_read_rgba8_aces(pt_ctx* ctx, unsigned char* host_dst, size_t bytes);
+/* Asynchronous presentation, for a loop that shows every frame (the reference draws each
+ * frame's texture, ogl_path_trace.h:189-192).  pt_present_begin(buf) enqueues the ACES
+ * epilogue of the image as of the renders issued so far, and its copy into the context's
+ * pinned host buffer `buf` (0..3) on a separate copy stream; it does not wait, and later
+ * renders overlap the copy.  pt_present_end(buf) waits for that copy and returns the
+ * rows_local * width RGBA8 pixels (same bytes as pt_read_rgba8_aces), valid until the next
+ * pt_present_begin on `buf` or pt_destroy.  Showing frame f-2 while frames f-1 and f render
+ * (three buffers in rotation) keeps two renders in flight, as the render-only loop does.
+ * A buffer begun again before its end first waits for its previous copy.
+ * PT_E_STATE: end without a begin. */
+int pt_present_begin(pt_ctx* ctx, int buf);
+int pt_present_end(pt_ctx* ctx, int buf, const unsigned char** pixels);
 /* Overwrites the local accumulation rows (resume from a checkpoint / seed a test). */
 int pt_write_rgba32f(pt_ctx* ctx, const float* host_src, size_t bytes);
 

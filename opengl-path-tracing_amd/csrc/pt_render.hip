@@ -1219,6 +1219,7 @@ constexpr int kTopNodes = 768;
 constexpr int kMaxSlots = 4, kAutoSlots = 2;
 constexpr size_t kQueueSet = kQueueStride;   // unsigned per queue head
 
+constexpr int kPresentBufs = 4;   // pt_present_begin buffers
 struct pt_ctx {
     pt_config cfg{};
     int rows_local = 0;
@@ -1297,6 +1298,13 @@ struct pt_ctx {
     float last_ms = 0.0f;
     unsigned long long last_counts[16] = {0};
     bool count_pending = false;
+    // asynchronous presentation (pt_present_begin / _end): per buffer a device RGBA8 image, a
+    // pinned host copy, its events, and one copy stream shared by the buffers
+    uchar4* present_dev[kPresentBufs] = {};
+    unsigned char* present_host[kPresentBufs] = {};
+    hipEvent_t ev_tonemap[kPresentBufs] = {}, ev_copied[kPresentBufs] = {};
+    bool present_pending[kPresentBufs] = {};
+    hipStream_t cstream = nullptr;
     std::string err;
 };
 
@@ -1409,6 +1417,14 @@ void pt_destroy(pt_ctx* c) {
         if (c->ev_adone[i]) (void)hipEventDestroy(c->ev_adone[i]);
     }
     if (c->ev_fence) (void)hipEventDestroy(c->ev_fence);
+    if (c->cstream) (void)hipStreamSynchronize(c->cstream);
+    for (int b = 0; b < kPresentBufs; b++) {
+        (void)hipFree(c->present_dev[b]);
+        if (c->present_host[b]) (void)hipHostFree(c->present_host[b]);
+        if (c->ev_tonemap[b]) (void)hipEventDestroy(c->ev_tonemap[b]);
+        if (c->ev_copied[b]) (void)hipEventDestroy(c->ev_copied[b]);
+    }
+    if (c->cstream) (void)hipStreamDestroy(c->cstream);
     for (auto& pr : c->ev_pending) { c->ev_free.push_back(pr.first); c->ev_free.push_back(pr.second); }
     for (hipEvent_t e : c->ev_free) (void)hipEventDestroy(e);
     if (c->stream) (void)hipStreamDestroy(c->stream);
@@ -2411,6 +2427,54 @@ int pt_read_rgba8_aces(pt_ctx* c, unsigned char* dst, size_t bytes) {
     HIPCHK(c, hipGetLastError());
     HIPCHK(c, hipStreamSynchronize(c->stream));
     HIPCHK(c, hipMemcpy(dst, c->rgba8, (size_t)n * 4, hipMemcpyDeviceToHost));
+    return PT_OK;
+}
+
+// Asynchronous presentation for a viewer that shows every frame (ogl_path_trace.h:189-192
+// draws each frame's texture on the GPU that rendered it; a headless caller reads it back).
+// begin: the ACES epilogue of the current image on the context stream (after every render
+// issued so far and its running mean), then a copy into pinned host memory on a separate
+// stream, so renders issued after it run while the image crosses PCIe.  end: waits for that
+// copy and hands out the pinned pixels.
+int pt_present_begin(pt_ctx* c, int buf) {
+    if (!c) return PT_E_ARG;
+    if (buf < 0 || buf >= kPresentBufs) return fail(c, PT_E_ARG, "present buffer must be 0..3");
+    const long long n = (long long)c->rows_local * c->cfg.width;
+    HIPCHK(c, hipSetDevice(c->cfg.device));
+    if (!c->cstream) HIPCHK(c, hipStreamCreateWithFlags(&c->cstream, hipStreamNonBlocking));
+    if (!c->present_dev[buf]) {
+        HIPCHK(c, hipMalloc(&c->present_dev[buf], std::max<long long>(n, 1) * sizeof(uchar4)));
+        HIPCHK(c, hipHostMalloc((void**)&c->present_host[buf], std::max<long long>(n, 1) * sizeof(uchar4),
+                                hipHostMallocDefault));
+        HIPCHK(c, hipEventCreateWithFlags(&c->ev_tonemap[buf], hipEventDisableTiming));
+        HIPCHK(c, hipEventCreateWithFlags(&c->ev_copied[buf], hipEventDisableTiming));
+    }
+    // a buffer begun again before its end: its previous copy must land first
+    if (c->present_pending[buf]) HIPCHK(c, hipEventSynchronize(c->ev_copied[buf]));
+    c->present_pending[buf] = false;
+    if (n > 0) {
+        hipLaunchKernelGGL(k_aces, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, c->stream, c->accum,
+                           c->present_dev[buf], n);
+        HIPCHK(c, hipGetLastError());
+    }
+    HIPCHK(c, hipEventRecord(c->ev_tonemap[buf], c->stream));
+    HIPCHK(c, hipStreamWaitEvent(c->cstream, c->ev_tonemap[buf], 0));
+    if (n > 0)
+        HIPCHK(c, hipMemcpyAsync(c->present_host[buf], c->present_dev[buf], (size_t)n * sizeof(uchar4),
+                                 hipMemcpyDeviceToHost, c->cstream));
+    HIPCHK(c, hipEventRecord(c->ev_copied[buf], c->cstream));
+    c->present_pending[buf] = true;
+    return PT_OK;
+}
+
+int pt_present_end(pt_ctx* c, int buf, const unsigned char** pixels) {
+    if (!c || !pixels) return PT_E_ARG;
+    if (buf < 0 || buf >= kPresentBufs) return fail(c, PT_E_ARG, "present buffer must be 0..3");
+    if (!c->present_pending[buf]) return fail(c, PT_E_STATE, "pt_present_end without pt_present_begin");
+    HIPCHK(c, hipSetDevice(c->cfg.device));
+    HIPCHK(c, hipEventSynchronize(c->ev_copied[buf]));
+    c->present_pending[buf] = false;
+    *pixels = c->present_host[buf];
     return PT_OK;
 }
 

@@ -101,6 +101,8 @@ def lib():
             "pt_read_rgba32f": (ip, [vp, vp, C.c_size_t]),
             "pt_read_rgba8_aces": (ip, [vp, vp, C.c_size_t]),
             "pt_write_rgba32f": (ip, [vp, vp, C.c_size_t]),
+            "pt_present_begin": (ip, [vp, ip]),
+            "pt_present_end": (ip, [vp, ip, C.POINTER(C.POINTER(C.c_ubyte))]),
             "pt_accum_device": (ip, [vp, C.POINTER(vp), C.POINTER(C.c_size_t)]),
             "pt_stream": (ip, [vp, C.POINTER(vp)]),
             "pt_set_counting": (ip, [vp, ip]),
@@ -381,6 +383,19 @@ class PathTracer:
         out = np.zeros((self.rows_local, self.width, 4), np.uint8)
         self._check(lib().pt_read_rgba8_aces(self.h, out.ctypes.data, out.nbytes))
         return out
+
+    def present_begin(self, buf):
+        """Enqueue the ACES RGBA8 image of the renders issued so far into pinned buffer buf
+        (0..3) without waiting (pt_present_begin)."""
+        self._check(lib().pt_present_begin(self.h, int(buf)))
+
+    def present_end(self, buf, copy=True):
+        """Wait for buffer buf and return its (rows_local, W, 4) uint8 pixels: a copy, or with
+        copy=False a view of the pinned buffer, valid until the next present_begin(buf)."""
+        ptr = C.POINTER(C.c_ubyte)()
+        self._check(lib().pt_present_end(self.h, int(buf), C.byref(ptr)))
+        view = np.ctypeslib.as_array(ptr, shape=(self.rows_local, self.width, 4))
+        return view.copy() if copy else view
 
     def accum_device(self):
         p, n = C.c_void_p(), C.c_size_t()

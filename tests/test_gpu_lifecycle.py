@@ -221,3 +221,40 @@ def test_overlap_slots_grow_and_switch(cornell_scene, slots):
     pt.close()
     assert f == 71
     assert_bitwise(got, want, "%d slots" % slots)
+
+
+@pytest.mark.parametrize("world,lag", [(1, 1), (1, 2), (3, 2)])
+def test_present_pipelined(cornell_scene, world, lag):
+    """pt_present_begin / _end: the reference's show-every-frame loop with the readback of
+    frame f-lag overlapping the renders of the later frames (lag + 1 pinned buffers in
+    rotation).  Every presented image equals the host ACES of the oracle's accumulation after
+    that frame, byte for byte, for each row-split rank; a buffer begun twice holds the later
+    image; misuse is refused."""
+    W, Hh, n = 72, 40, 7
+    want = [H.aces_rgba8_host(O.render(cornell_scene, W, Hh, max_bounce=6, n_frames=f)) for f in range(1, n + 1)]
+    nb = lag + 1
+    for rank in range(world):
+        pt = H.PathTracer(W, Hh, max_bounce=6, rank=rank, world=world)
+        pt.upload(cornell_scene)
+        got = []
+        for i in range(n):
+            pt.render_async(i + 1, 1, 0 if i == 0 else 1)
+            pt.present_begin(i % nb)
+            if i >= lag:
+                got.append(pt.present_end((i - lag) % nb))
+        for j in range(n - lag, n):
+            got.append(pt.present_end(j % nb))
+        for f, img in enumerate(got, 1):
+            assert np.array_equal(img, want[f - 1][rank::world]), (rank, f)
+        assert np.array_equal(pt.read_rgba8(), want[-1][rank::world])
+        # begun twice without an end: the later image
+        pt.present_begin(0)
+        pt.render(n + 1, 1, 1)
+        pt.present_begin(0)
+        last = H.aces_rgba8_host(O.render(cornell_scene, W, Hh, max_bounce=6, n_frames=n + 1))
+        assert np.array_equal(pt.present_end(0, copy=False), last[rank::world])
+        with pytest.raises(H.PTError):
+            pt.present_end(0)          # no begin pending
+        with pytest.raises(H.PTError):
+            pt.present_begin(4)
+        pt.close()

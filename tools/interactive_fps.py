@@ -1,7 +1,10 @@
 """Interactive-loop rate: the reference's render loop -- one dispatch per
 displayed frame, ogl_path_trace.h:160-204 -- through pt_viewer_frame (pt_render_async, like
 glDispatchCompute), with and without the per-frame readback a window would upload (the ACES
-RGBA8 view or the raw RGBA32F accumulation; a readback waits for its frame).  Each row is run
+RGBA8 view or the raw RGBA32F accumulation; a readback waits for its frame; rgba8_present_L
+is the pipelined ACES view through pt_present_begin / _end, the host showing frame f-L while
+the later frames render and frame f-L+1's image crosses PCIe into pinned memory, L+1
+buffers in rotation).  Each row is run
 with the overlapped short launches on (default) and off (tuning key 9).  Scene and accumulator
 stay in HBM.  One GPU.
 
@@ -26,7 +29,7 @@ def main():
     ap.add_argument("--frames", type=int, default=300)
     ap.add_argument("--bounces", type=int, default=8)
     ap.add_argument("--scene", default="cornell")
-    ap.add_argument("--rows", default="none,rgba8_aces,rgba32f")
+    ap.add_argument("--rows", default="none,rgba8_aces,rgba8_present_1,rgba8_present_2,rgba32f")
     ap.add_argument("--combos", default="9=0;9=1",
                     help="tuning settings to run, ';'-separated, each a ','-list of key=value (pt_set_tuning); "
                          "row suffix: '' for 9=0 (automatic overlap), '_no_overlap' for 9=1, else the settings")
@@ -62,8 +65,17 @@ def main():
                 v.frame(pt, 1.0 + 0.001 * i)                  # enqueued, like glDispatchCompute
                 if readback == "rgba8_aces":
                     pt.read_rgba8()
+                elif readback.startswith("rgba8_present_"):
+                    lag = int(readback.rsplit("_", 1)[1])
+                    pt.present_begin(i % (lag + 1))
+                    if i >= lag:                                  # frame i-lag, shown while later ones render
+                        pt.present_end((i - lag) % (lag + 1), copy=False)
                 elif readback == "rgba32f":
                     pt.read_rgba32f()
+            if readback.startswith("rgba8_present_"):
+                lag = int(readback.rsplit("_", 1)[1])
+                for j in range(max(0, a.frames - lag), a.frames):
+                    pt.present_end(j % (lag + 1), copy=False)
             pt.sync()
             dt = time.perf_counter() - t0
             v.close()
