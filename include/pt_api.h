@@ -154,7 +154,8 @@ int pt_set_kernel(pt_ctx* ctx, int variant);
  * key 3 = resident waves per SIMD the kernel is compiled for (5..8; 0 = auto: 7 for scenes
  *         staged in LDS, 6 for global-memory scenes),
  * key 4 = queue ids a wave reserves per queue atomic in frame-split mode (1..1024; 0 = auto:
- *         128 / 64 for LDS-staged scenes with items of 1 / 2 frames, else 32).
+ *         256 / 64 for LDS-staged scenes with items of 1 / 2 frames, else about the launch's
+ *         queue ids per resident wave / (8 x frames per item), clamped to 32..256).
  * key 5 = frames per work item (>= 1; 0 = auto, 2..8): a pixel's frames are spread over
  *         several lanes and the running mean is applied by a second kernel in frame order;
  *         a value >= n_frames gives each lane whole pixels (running mean in registers).

@@ -2038,10 +2038,22 @@ static int enqueue_render(pt_ctx* c, int frame_first, int n_frames, int acc_firs
     // items and the global-memory scenes' long segments keep 32 (C3 stand-in, one frame per
     // launch: 3.19 ms with 32, 3.63 with 128).  With overlapped one-frame launches (2 slots)
     // 256 ids beat 128 (0.594 vs 0.603 ms per 1080p frame; 64: 0.689).  Tuning key 4 overrides.
+    //
+    // Otherwise (round 3 sweep, same process) the best reservation follows the queue ids a
+    // resident wave takes over the launch, I, and the frames per item, g: about I / (8 g),
+    // between 32 and 256.  Global-memory scenes (C3 stand-in): one-frame launches best at 48
+    // (+4% over 32), 4-frame 128 (+3.8%), 8-frame 64 (+1.9%), 16-frame 32, 32-frame 64 (+1%),
+    // 64-frame 128 (+1.3%), 256-frame 192-256 (+2.2%; C4 +2.1%); C2's 1024-frame launch 128
+    // (+0.9%).  Fewer ids per wave than that make the queue atomic's round trip frequent;
+    // more leave the last waves holding a long reservation in the launch tail.
     {
         const bool lds_items = lds_staged(c);
+        const double waves = (double)c->n_cu * 4.0 * (lds_items ? 7.0 : 6.0);
+        const double ids = (double)c->n_tiles * (double)((n_frames + p.group - 1) / p.group) * 64.0;
+        const int fit = 16 * (int)(ids / std::max(waves, 1.0) / (8.0 * p.group) / 16.0 + 0.5);
+        const int auto_batch = std::max((int)kPullBatch, std::min(256, fit));
         p.pull_batch = c->pull_batch ? c->pull_batch
-                                     : (lds_items && p.group <= 2 ? (p.group == 1 ? 256 : 64) : (int)kPullBatch);
+                                     : (lds_items && p.group <= 2 ? (p.group == 1 ? 256 : 64) : auto_batch);
     }
     {   // exact item / n_groups by ceil(2^32 / n_groups) when item * n_groups < 2^32 for every
         // item (then floor(item * m / 2^32) = floor(item / n_groups)), else the division

@@ -5,6 +5,11 @@ round, so clock and thermal drift between processes does not enter the compariso
 python tools/ab_inproc.py --libs base,cur --rounds 4 --spp 128 --chunk 128 [--scene bunny [--tris 300]]
 ('cur' = build/libptrace.so, other names = build/libptrace_<name>.so from tools/ab_build.sh;
  an entry name:k=v[:k=v] adds pt_set_tuning keys for that entry only, e.g. --libs cur,p37:3=8)
+
+Launches of at most 16 frames run overlapped on extra streams (tuning key 9), and the contexts
+of every build after the first then share the process's hardware queues (GPU_MAX_HW_QUEUES=4)
+with the first's: measured 15-25% slower whichever build comes second.  Compare such launch
+shapes one build per process (or with --key 9=1 for all).
 """
 import argparse
 import importlib.util
@@ -45,6 +50,9 @@ def main():
     ap.add_argument("--key", action="append", default=[], help="pt_set_tuning key=value for every build (repeatable)")
     a = ap.parse_args()
     libs = a.libs.split(",")
+    if len(libs) > 1 and min(a.chunk, a.spp) <= 16 and not any(k.startswith("9=") for k in a.key):
+        print("warning: overlapped short launches of several builds share hardware queues; the order "
+              "biases the result (run one build per process, or --key 9=1)", flush=True)
     mods = {}
     for l in libs:
         name = l.split(":")[0]
