@@ -267,6 +267,9 @@ extern __shared__ float4 g_lds[];   // the state-machine kernel's scene copy (no
 #ifndef PT_PAD_NODES
 #define PT_PAD_NODES 67
 #endif
+#ifndef PT_GWALK_FLAT
+#define PT_GWALK_FLAT 1
+#endif
 constexpr int kPadNodes = PT_PAD_NODES;
 typedef float v4f __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) const v4f lds_v4f;
@@ -648,6 +651,21 @@ __device__ __forceinline__ void trav_walk(const SceneView& S, f3 o, f3 d, f3 rd,
     }
 #endif
     auto step = [&]() {
+#if PT_GWALK_FLAT
+        if (!LDS && !COUNT && ALL_FAST) {
+            // global-memory walk without the per-step exec-mask branch: a lane whose walk has
+            // stopped (w < 0) steps on the root, an LDS top node (S.np >= 1 for any tree), and
+            // keeps its w and leaf
+            const bool on = w >= 0;
+            float4 lo, hi;
+            node_at<LDS, PADN>(S, on ? w : 0, lo, hi);
+            const int a = __float_as_int(hi.z), b = __float_as_int(hi.w);
+            const bool hb = slab_fast(lo, hi, o, d, rd, t);
+            leaf = on ? a : leaf;
+            w = on ? (hb ? (a >= 0 ? a : -3 - b) : b) : w;
+            return;
+        }
+#endif
         if (w >= 0) {
             float4 lo, hi;
             node_at<LDS, PADN>(S, w, lo, hi);
