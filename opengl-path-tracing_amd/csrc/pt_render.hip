@@ -267,6 +267,12 @@ extern __shared__ float4 g_lds[];   // the state-machine kernel's scene copy (no
 #ifndef PT_PAD_NODES
 #define PT_PAD_NODES 67
 #endif
+#ifndef PT_FLAGS_IN_STATE
+#define PT_FLAGS_IN_STATE 1
+#endif
+#ifndef PT_FAST_FROM_RD
+#define PT_FAST_FROM_RD 1
+#endif
 #ifndef PT_GWALK_FLAT
 #define PT_GWALK_FLAT 1
 #endif
@@ -802,11 +808,21 @@ __global__ __launch_bounds__(NT, MINW) void k_render_sm(KParams p) {
 
     Cnt c = {0, 0, 0, 0, 0};
     int st = ST_SHADE;
+#if PT_FLAGS_IN_STATE
+    // "fresh" (SHADE without a segment to finish: start / after shading) is t < 0, and "a new
+    // camera ray is due" is bounce < 0: no lane-mask booleans carried around the loop (their
+    // merges cost scalar instructions on every iteration)
+#define PT_FRESH (t < 0.0f)
+#define PT_NEED_RAY (bounce < 0)
+#else
     bool fresh = true;        // SHADE without a finished segment (start / after fetch)
     bool need_ray = true;     // next SHADE must start a new camera ray
+#define PT_FRESH fresh
+#define PT_NEED_RAY need_ray
+#endif
     int lx = -1, y = 0;
     int aidx = 0;             // rows_local * W < 2^31 (checked at pt_create)
-    int k = 0, kend = 0, r = 0, bounce = 0;   // frames k..kend-1 of this work item
+    int k = 0, kend = 0, r = 0, bounce = PT_FLAGS_IN_STATE ? -1 : 0;   // frames k..kend-1 of this work item
     unsigned qnext = 0, qend = 0;             // wave's reserved queue ids (frame-split mode)
     unsigned tile_id = 0, pcost = 0;    // adaptive queue order: this pixel's tile + segments
     float4 acc = make_float4(0, 0, 0, 0);
@@ -817,15 +833,22 @@ __global__ __launch_bounds__(NT, MINW) void k_render_sm(KParams p) {
     // the reference performs when it accepts the hit (o + d*t; the stored/recomputed
     // normal and its flip against d; matIdx), on the same final t -- the same bits.
     //   hprim >= 0: triangle slot, -1: no hit, <= -2: sphere (-2 - index)
+#if !PT_FAST_FROM_RD
     bool fast = false;
+#endif
     f3 rd = mk(0, 0, 0);
-    float t = 0.0f;
+    float t = PT_FLAGS_IN_STATE ? -1.0f : 0.0f;
     int hprim = -1, bi = -1, leaf = 0;   // bi: walk position (WalkLinks); leaf: code of a hit leaf
 
 #ifdef PT_PHASE_CLOCK
     unsigned long long clk[6] = {0, 0, 0, 0, 0, 0};   // cycles + wave iterations per phase
 #endif
     for (;;) {
+#if PT_FAST_FROM_RD
+        // inside the exact-reciprocal guard (the segment's "fast" walk) <=> rd was set: |d_i| is
+        // in [2^-20, 2] there, so RN(1/d_x) is nonzero; outside it rd stays 0
+        const bool fast = rd.x != 0.0f;
+#endif
         int nS = __popcll(__ballot(st == ST_SHADE));
         int nL = __popcll(__ballot(st == ST_LEAF));
         int nT = __popcll(__ballot(st == ST_TRAV));
@@ -842,7 +865,7 @@ __global__ __launch_bounds__(NT, MINW) void k_render_sm(KParams p) {
         const bool low = nT < p.trav_floor;
         if (nS > 0 && (nS >= p.shade_thresh || (low && nL == 0))) {
             // ---------------- SHADE: finish segment, regenerate, set up next segment
-            if (st == ST_SHADE && !fresh) {
+            if (st == ST_SHADE && !PT_FRESH) {
                 const bool hit = hprim != -1;
                 if (COUNT) { c.seg++; if (hit) c.hits++; diag_tick(c.sw, c.sl); }
                 pcost++;
@@ -904,7 +927,11 @@ __global__ __launch_bounds__(NT, MINW) void k_render_sm(KParams p) {
                     rgb = inc + env * col;
                     finished = true;
                 }
+#if PT_FLAGS_IN_STATE
+                if (finished) bounce = -1;
+#else
                 need_ray = finished;
+#endif
                 if (finished) {
                     bool frame_done = true;
                     f3 px;
@@ -932,9 +959,13 @@ __global__ __launch_bounds__(NT, MINW) void k_render_sm(KParams p) {
                         k++;
                     }
                 }
+#if PT_FLAGS_IN_STATE
+                t = -1.0f;
+#else
                 fresh = true;
+#endif
             }
-            if ((st == ST_SHADE) & need_ray & (lx >= 0) & (k >= (SPLIT ? kend : p.n_frames))) {
+            if ((st == ST_SHADE) & PT_NEED_RAY & (lx >= 0) & (k >= (SPLIT ? kend : p.n_frames))) {
                 if (!SPLIT) p.accum[aidx] = acc;
                 if (p.tile_cost && tile_id != ~0u) atomicAdd(&p.tile_cost[tile_id], pcost);
                 lx = -1;
@@ -1005,13 +1036,17 @@ __global__ __launch_bounds__(NT, MINW) void k_render_sm(KParams p) {
                             r = 0;
                             psum = mk(0, 0, 0);
                             if (!SPLIT) acc = p.acc_first ? p.accum[aidx] : make_float4(0, 0, 0, 0);
+#if PT_FLAGS_IN_STATE
+                            bounce = -1;
+#else
                             need_ray = true;
+#endif
                         }
                     }
                 }
             }
             if (st == ST_SHADE && lx >= 0) {
-                if (need_ray) {       // camera ray (:514-542)
+                if (PT_NEED_RAY) {    // camera ray (:514-542)
                     if (r == 0) state = pt::seed(lx, y, p.frame_first + k);
                     float ax = 0.0f, ay = 0.0f;
                     if (!(p.flags & PT_FLAG_NO_AA)) {
@@ -1028,18 +1063,33 @@ __global__ __launch_bounds__(NT, MINW) void k_render_sm(KParams p) {
                     inc = mk(0, 0, 0);
                     col = mk(1, 1, 1);
                     bounce = 0;
+#if !PT_FLAGS_IN_STATE
                     need_ray = false;
+#endif
                 }
                 // segment set-up: exact-reciprocal guard, spheres (:372-385), walk start
                 // the ray half of the guard, evaluated without short-circuit branches (each
                 // && of the old form was an exec-mask branch): every origin component 0 or
                 // in [2^-40, 2^60], every direction component in [2^-20, 2] (NaN fails)
-                fast = (p.scene_fast != 0) & in_guard(o.x, 0x1p-40f, 0x1p60f) & in_guard(o.y, 0x1p-40f, 0x1p60f) &
+#if PT_FAST_FROM_RD
+                const bool fast_seg =
+#else
+                fast =
+#endif
+                       (p.scene_fast != 0) & in_guard(o.x, 0x1p-40f, 0x1p60f) & in_guard(o.y, 0x1p-40f, 0x1p60f) &
                        in_guard(o.z, 0x1p-40f, 0x1p60f) & in_range_abs(d.x, 0x1p-20f, 2.0f) &
                        in_range_abs(d.y, 0x1p-20f, 2.0f) & in_range_abs(d.z, 0x1p-20f, 2.0f);
+#if PT_FAST_FROM_RD
+#define PT_FAST_SEG fast_seg
+                // under the guard |d_i| is in [2^-20, 2]: rcp_fast is the exact RN(1/d_i); rd = 0
+                // marks a segment outside it
+                rd = fast_seg ? mk(pt::rcp_fast(d.x), pt::rcp_fast(d.y), pt::rcp_fast(d.z)) : mk(0, 0, 0);
+#else
+#define PT_FAST_SEG fast
                 // under the guard |d_i| is in [2^-20, 2]: rcp_fast is the exact RN(1/d_i)
                 if (fast) rd = mk(pt::rcp_fast(d.x), pt::rcp_fast(d.y), pt::rcp_fast(d.z));
-                if (COUNT && !fast) c.slow++;
+#endif
+                if (COUNT && !PT_FAST_SEG) c.slow++;
                 if (COUNT && ray_has_nan(o, d)) c.nan++;
                 t = __builtin_huge_valf();
                 hprim = -1;
@@ -1059,14 +1109,16 @@ __global__ __launch_bounds__(NT, MINW) void k_render_sm(KParams p) {
                         }
                     }
                 }
+#if !PT_FLAGS_IN_STATE
                 fresh = false;
+#endif
                 const bool walk = use_tris & (COUNT || !ray_has_nan(o, d));
                 // inside the root box (all three axes, inclusive) each axis has near <= 0 <=
                 // far, so the exact slab says hit for any t >= 0: skip the root's test
-                const bool inside = (root_skip >= 0) & fast & (o.x >= p.root_box[0]) & (o.x <= p.root_box[1]) &
+                const bool inside = (root_skip >= 0) & PT_FAST_SEG & (o.x >= p.root_box[0]) & (o.x <= p.root_box[1]) &
                                     (o.y >= p.root_box[2]) & (o.y <= p.root_box[3]) & (o.z >= p.root_box[4]) &
                                     (o.z <= p.root_box[5]);
-                const int img = (LDS && fast) ? oct_base(d, S.np << 5) : 0;   // octant image
+                const int img = (LDS && PT_FAST_SEG) ? oct_base(d, S.np << 5) : 0;   // octant image
                 bi = walk ? (inside ? root_skip : 0) + img : -1;
                 st = walk ? ST_TRAV : ST_SHADE;
             }
