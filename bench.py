@@ -87,7 +87,8 @@ def main():
     ap.add_argument("--height", type=int, default=None)
     ap.add_argument("--bounces", type=int, default=None)
     ap.add_argument("--variant", type=int, default=0)
-    ap.add_argument("--cpu-spp", type=int, default=2, help="spp of the bounded CPU-baseline sample")
+    ap.add_argument("--cpu-spp", type=int, default=20,
+                    help="spp of the bounded CPU-baseline sample (20: about 10 s on a 16-CPU share)")
     ap.add_argument("--cpu-threads", type=int, default=0, help="0 = every CPU this process may use")
     ap.add_argument("--no-cold", action="store_true", help="skip the cold first-render measurement")
     ap.add_argument("--no-cpu-baseline", action="store_true")
