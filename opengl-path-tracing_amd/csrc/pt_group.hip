@@ -24,9 +24,12 @@
 #include <string>
 #include <vector>
 
-// internal hook of pt_render.hip (not part of the public ABI)
-extern "C" int pt__scene_replicate_layout(pt_ctx* dst, const pt_ctx* src, void* dptr[6], const void* sptr[6],
-                                          size_t bytes[6]);
+// internal hooks of pt_render.hip (not part of the public ABI): kSceneBufs device scene
+// buffers of a context, and the flag that lets a replicated context render
+constexpr int kSceneBufs = 10;
+extern "C" int pt__scene_replicate_layout(pt_ctx* dst, const pt_ctx* src, void* dptr[kSceneBufs],
+                                          const void* sptr[kSceneBufs], size_t bytes[kSceneBufs]);
+extern "C" int pt__scene_set_ready(pt_ctx* c, int ready);
 
 namespace {
 
@@ -127,6 +130,11 @@ int pt_group_create(pt_ctx* const* ctxs, int n, pt_group** out) {
     for (int i = 0; i < n; i++) {
         if (cfg[i].width != g->W || cfg[i].height != g->H || cfg[i].world != g->world)
             return gfail(g, PT_E_ARG, "contexts of one group need the same width, height and world");
+        // the gathered frame is one render only if every context renders the same way
+        if (cfg[i].max_bounce != cfg[0].max_bounce || cfg[i].display_mode != cfg[0].display_mode ||
+            cfg[i].flags != cfg[0].flags || cfg[i].rays_per_pixel != cfg[0].rays_per_pixel)
+            return gfail(g, PT_E_ARG, "contexts of one group need the same max_bounce, display_mode, flags and "
+                                      "rays_per_pixel");
         if (cfg[i].rank < 0 || cfg[i].rank >= n || seen[cfg[i].rank]++)
             return gfail(g, PT_E_ARG, "context ranks must be 0..world-1, each once");
     }
@@ -183,9 +191,11 @@ int pt_group_upload_scene(pt_group* g, const float* tris, int n_tris, const floa
     int rc = pt_upload_scene(root, tris, n_tris, bvh, n_nodes, mats, n_mats, spheres, n_spheres);
     if (rc) return gfail(g, rc, std::string("pt_upload_scene: ") + pt_last_error(root));
     const int n = (int)g->ctx.size(), nd = (int)g->devs.size();
-    std::vector<std::vector<void*>> dptr(n, std::vector<void*>(6, nullptr));
-    const void* sptr[6] = {nullptr};
-    size_t bytes[6] = {0};
+    std::vector<std::vector<void*>> dptr(n, std::vector<void*>(kSceneBufs, nullptr));
+    const void* sptr[kSceneBufs] = {nullptr};
+    size_t bytes[kSceneBufs] = {0};
+    // the replicated contexts render only once their buffers are filled (set below, after the
+    // streams have drained without error)
     for (int i = 1; i < n; i++) {
         rc = pt__scene_replicate_layout(g->ctx[i], root, dptr[i].data(), sptr, bytes);
         if (rc) return gfail(g, rc, std::string("scene layout: ") + pt_last_error(g->ctx[i]));
@@ -195,7 +205,7 @@ int pt_group_upload_scene(pt_group* g, const float* tris, int n_tris, const floa
     std::vector<int> leader(nd, -1);
     for (int i = 0; i < n; i++)
         if (leader[g->dev_idx[i]] < 0) leader[g->dev_idx[i]] = i;
-    for (int b = 0; b < 6; b++) {
+    for (int b = 0; b < kSceneBufs; b++) {
         if (!bytes[b]) continue;
         if (nd > 1) {
             GNCCL(g, ncclGroupStart());
@@ -219,6 +229,7 @@ int pt_group_upload_scene(pt_group* g, const float* tris, int n_tris, const floa
         GHIP(g, hipSetDevice(g->devs[d]));
         GHIP(g, hipStreamSynchronize(g->stream[d]));
     }
+    for (int i = 1; i < n; i++) pt__scene_set_ready(g->ctx[i], 1);
     return PT_OK;
 }
 
@@ -228,19 +239,30 @@ int pt_group_gather_rgba32f(pt_group* g, float* dst, size_t bytes, int dst_on_de
     if (bytes < frame_bytes) return gfail(g, PT_E_ARG, "destination too small");
     const int n = (int)g->ctx.size(), nd = (int)g->devs.size();
     const size_t blk = block_floats(g);
-    GHIP(g, hipSetDevice(g->devs[0]));
-    GHIP(g, hipEventRecord(g->ev0, g->stream[0]));
-    // pack: each context's rows into its block, after its stream's pending renders
+    // the device streams wait for every context's pending renders first; the timer starts
+    // after those waits, at the first pack copy (pt_group.h), not while renders still run
     for (int i = 0; i < n; i++) {
         const int d = g->dev_idx[i];
         void* cs = nullptr;
-        void* acc = nullptr;
-        size_t ab = 0;
         pt_stream(g->ctx[i], &cs);
-        pt_accum_device(g->ctx[i], &acc, &ab);
         GHIP(g, hipSetDevice(g->devs[d]));
         GHIP(g, hipEventRecord(g->ctx_ev[i], (hipStream_t)cs));
         GHIP(g, hipStreamWaitEvent(g->stream[d], g->ctx_ev[i], 0));
+    }
+    for (int i = 0; i < n; i++) {   // the root stream also waits for the other devices' renders
+        if (g->dev_idx[i] == 0) continue;
+        GHIP(g, hipSetDevice(g->devs[0]));
+        GHIP(g, hipStreamWaitEvent(g->stream[0], g->ctx_ev[i], 0));
+    }
+    GHIP(g, hipSetDevice(g->devs[0]));
+    GHIP(g, hipEventRecord(g->ev0, g->stream[0]));
+    // pack: each context's rows into its block
+    for (int i = 0; i < n; i++) {
+        const int d = g->dev_idx[i];
+        void* acc = nullptr;
+        size_t ab = 0;
+        pt_accum_device(g->ctx[i], &acc, &ab);
+        GHIP(g, hipSetDevice(g->devs[d]));
         if (ab) GHIP(g, hipMemcpyAsync(g->send[d] + (size_t)g->slot[i] * blk / 4, acc, ab, hipMemcpyDeviceToDevice,
                                        g->stream[d]));
     }

@@ -21,6 +21,7 @@
 //   mat   48 B : {color.rgb, smoothness}, {emission*strength, specProb}, {specular.rgb, 0}
 //   sphere 32 B: {c.xyz, r*r}, {matIdx, 0, 0, 0}
 #include "pt_math.h"
+#include "pt_wide.h"
 #include "../../include/pt_api.h"
 #include "../../include/pt_scene.h"
 
@@ -45,6 +46,10 @@ struct DevScene {
     const float4* tris;
     const float4* mats;
     const float4* spheres;
+    // the 4-wide quantised tree of the global-memory walk (pt_wide.h): records (4 float4 per
+    // index) and the exact leaf boxes (2 float4 per index, axis-paired like the node records)
+    const float4* wrec;
+    const float4* wlbox;
     int n_nodes, n_spheres;
 };
 
@@ -88,6 +93,8 @@ struct KParams {
     int shade_lds;                 // global-memory scene: materials + spheres staged in LDS too
     int cons_walk;                 // LDS scene: the culling walk (slab_oct_cons, exact leaf re-test)
     float cons_m[3];               // ... 2^-19 * the scene's largest |coordinate| per axis, rounded up
+    int wide_top;                  // wide walk (WIDE instantiations): records [0, wide_top) staged in LDS
+    float wide_cw[3];              // ... 2^-18 * the scene's largest |coordinate| per axis, rounded up (WRay)
 };
 
 // Progressive mode (hipGraph replay): the frame range comes from a device counter, and
@@ -237,6 +244,10 @@ struct SceneView {
     const float4* spheres;
     int np, tp;    // plane strides (float4) of the state-machine kernel's LDS copy
     float cm[3];   // culling walk: 2^-19 * the scene's largest |coordinate| per axis (slab_oct_cons)
+    const float4* wrec;    // wide walk: records (global), their first `wtop` staged in LDS planes
+    const float4* wlbox;   // ... exact leaf boxes
+    int wtop;
+    float cw[3];
 };
 
 // Node / triangle-record access of the state-machine kernel.  Global memory holds AoS
@@ -587,7 +598,8 @@ __device__ __forceinline__ void trav_walk(const SceneView& S, f3 o, f3 d, f3 rd,
                                           unsigned long long live, unsigned long long m_trav,
                                           unsigned long long m_leaf, unsigned long long m_shade,
                                           int leaf_thresh, int shade_thresh,
-                                          int trav_floor, int& st, int& bi, int& leaf, Cnt& c) {
+                                          int trav_floor, int& st, int& bi, int& leaf, Cnt& c,
+                                          bool eligible = true) {
     const int min_thresh = leaf_thresh < shade_thresh ? leaf_thresh : shade_thresh;
     f3 ol = mk(0, 0, 0), oh = mk(0, 0, 0);
     float E = 0.0f;
@@ -612,7 +624,9 @@ __device__ __forceinline__ void trav_walk(const SceneView& S, f3 o, f3 d, f3 rd,
     // LDS walks take the lane masks of the three states from the phase choice (uniform values:
     // no per-lane booleans copied into the walk loop, +1.2..1.5% on C2); the global-memory walk
     // measured 0.8-1% slower that way and keeps its own ballots
-    const bool walking = st == ST_TRAV;
+    // (eligible: the wide walk's scenes send only the lanes outside the exact-reciprocal guard
+    // here, and the walking lanes inside it wait)
+    const bool walking = (st == ST_TRAV) & eligible;
     const unsigned long long mw = LDS ? m_trav : __ballot(walking);
     const unsigned long long pre_leaf = LDS ? m_leaf : __ballot(st == ST_LEAF);
     const unsigned long long pre_shade = LDS ? m_shade : __ballot(st == ST_SHADE);
@@ -726,6 +740,74 @@ __device__ __forceinline__ void trav_walk(const SceneView& S, f3 o, f3 d, f3 rd,
     }
 }
 
+// ------------------------------------------------------------------ the wide walk
+// Global-memory scenes whose tree is nested (pt_bvh_culling_ok) walk the 4-wide quantised tree
+// of pt_wide.h: one 48-B record per step tests up to four descendants
+// conservatively, and the lane keeps a two-entry stack of pending children plus a resume
+// position.  Lanes inside the exact-reciprocal guard only; their leaf boxes are re-tested
+// exactly in the leaf phase before a triangle may move t.  The first `wtop` records sit in
+// LDS as three planes (q0 at [i], q1 at [wtop + i], q2 at [2 wtop + i]).
+constexpr int kWideStack = 2;
+#ifndef PT_WIDE_UNROLL
+#define PT_WIDE_UNROLL 2
+#endif
+__device__ __forceinline__ void wrec_at(const SceneView& S, int n, float4& q0, float4& q1, float4& q2) {
+    if (n < S.wtop) {
+        const unsigned b = (unsigned)n << 4, k = (unsigned)S.wtop << 4;
+        const v4f x = *(lds_v4f*)(size_t)b;
+        const v4f y = *(lds_v4f*)(size_t)(b + k);
+        const v4f z = *(lds_v4f*)(size_t)(b + 2u * k);
+        q0 = make_float4(x.x, x.y, x.z, x.w);
+        q1 = make_float4(y.x, y.y, y.z, y.w);
+        q2 = make_float4(z.x, z.y, z.z, z.w);
+    } else {
+        const float4* r = S.wrec + 4 * n;
+        q0 = r[0];
+        q1 = r[1];
+        q2 = r[2];
+    }
+}
+
+// The TRAV phase of the wide walk (every walking lane inside the guard): each lane visits one
+// record per step (ptw::wide_hits + wide_visit, the functions the CPU model in
+// tests/wide/wide_sim.cpp checks against the reference walk) until it stops at a leaf (-> LEAF)
+// or its walk ends (-> SHADE).  Stopped lanes step on record 0 (in LDS) without changing their
+// state.  The yield rule is trav_walk's.
+__device__ __forceinline__ void trav_wide(const SceneView& S, f3 o, f3 rd, float t, unsigned long long live,
+                                          int leaf_thresh, int shade_thresh, int trav_floor, int& st, int& bi,
+                                          uint32_t (&e)[kWideStack], int& R) {
+    const int min_thresh = leaf_thresh < shade_thresh ? leaf_thresh : shade_thresh;
+    const ptw::WRay wr = ptw::make_wray(o, rd, S.cw, rd.x < 0.0f, rd.y < 0.0f, rd.z < 0.0f);
+    const bool walking = st == ST_TRAV;
+    const unsigned long long mw = __ballot(walking);
+    const unsigned long long pre_leaf = __ballot(st == ST_LEAF), pre_shade = __ballot(st == ST_SHADE);
+    int cur = walking ? bi : -1;
+    const int floor1 = trav_floor > 1 ? trav_floor : 1;
+    const int wait_lim = __popcll(live) - min_thresh;
+    for (;;) {
+#pragma unroll
+        for (int u = 0; u < PT_WIDE_UNROLL; u++) {
+            const bool on = cur >= 0;
+            float4 q0, q1, q2;
+            wrec_at(S, on ? cur >> 3 : 0, q0, q1, q2);
+            const uint32_t pend = ptw::wide_hits(q0.x, q0.y, q0.z, __float_as_uint(q0.w), __float_as_uint(q1.x),
+                                                 __float_as_uint(q1.y), __float_as_uint(q1.z), __float_as_uint(q1.w),
+                                                 __float_as_uint(q2.x), __float_as_uint(q2.y), wr, t, cur & 7);
+            if (on) cur = ptw::wide_visit<kWideStack>(cur, pend, __float_as_int(q2.z), __float_as_int(q2.w), e, R);
+        }
+        const int nw = __popcll(__ballot(cur >= 0));
+        if (nw < floor1) break;
+        if (nw <= wait_lim) {
+            if (__popcll(pre_leaf | __ballot(cur <= -2)) >= leaf_thresh) break;
+            if (__popcll(pre_shade | (__ballot(cur == -1) & mw)) >= shade_thresh) break;
+        }
+    }
+    if (walking) {
+        st = cur >= 0 ? ST_TRAV : (cur == -1 ? ST_SHADE : ST_LEAF);
+        bi = cur;
+    }
+}
+
 #ifdef PT_PHASE_CLOCK
 // experiment builds only (tools/ab_build.sh with PT_EXTRA=-DPT_PHASE_CLOCK): per-phase
 // wave-clock accounting of the state machine, read back by pt_debug_phase_clock
@@ -740,8 +822,9 @@ constexpr int kWaveTraceMax = 16384;
 __device__ unsigned long long g_wave_trace[kWaveTraceMax * 4];
 #endif
 
-template <bool COUNT, bool LDS, int MINW, bool MULTI, bool SPLIT, bool PADN = false, int NT = 256>
+template <bool COUNT, bool LDS, int MINW, bool MULTI, bool SPLIT, bool PADN = false, int NT = 256, bool WIDE = false>
 __global__ __launch_bounds__(NT, MINW) void k_render_sm(KParams p) {
+    static_assert(!WIDE || (!LDS && !COUNT), "the wide walk is the global-memory walk of a render build");
 #ifdef PT_WAVE_TRACE
     const unsigned long long wt_entry = __builtin_amdgcn_s_memrealtime();
     unsigned wt_items = 0;
@@ -777,22 +860,35 @@ __global__ __launch_bounds__(NT, MINW) void k_render_sm(KParams p) {
         S.tris = p.sc.tris;
         S.mats = p.sc.mats;
         S.spheres = p.sc.spheres;
-        // the top nodes (breadth-first numbering) in LDS planes: lo at [i], hi at [n_top + i]
+        S.wrec = p.sc.wrec;
+        S.wlbox = p.sc.wlbox;
+        S.cw[0] = p.wide_cw[0];
+        S.cw[1] = p.wide_cw[1];
+        S.cw[2] = p.wide_cw[2];
         if ((unsigned)(size_t)(__attribute__((address_space(3))) const char*)g_lds != 0u) __builtin_trap();
-        const int K = p.n_top;
-        for (int i = threadIdx.x; i < 2 * K; i += blockDim.x) lds[(i & 1) * K + (i >> 1)] = p.sc.nodes[i];
+        // the top nodes (breadth-first numbering) in LDS planes: lo at [i], hi at [n_top + i];
+        // the wide walk stages its top records instead (wrec_at), and the binary walk of its
+        // lanes outside the guard reads every node from global memory
+        const int K = WIDE ? p.wide_top : p.n_top;
+        if (WIDE) {
+            for (int i = threadIdx.x; i < 3 * K; i += blockDim.x) lds[(i % 3) * K + i / 3] = p.sc.wrec[4 * (i / 3) + i % 3];
+        } else {
+            for (int i = threadIdx.x; i < 2 * K; i += blockDim.x) lds[(i & 1) * K + (i >> 1)] = p.sc.nodes[i];
+        }
+        const int KQ = WIDE ? 3 * K : 2 * K;   // float4 before the shading records
         // materials and spheres after them when small (p.shade_lds): every segment's sphere
         // test and every hit's material then read LDS, not scattered global lines (the global
         // walk is bound by its vector-memory lane-loads)
         if (p.shade_lds) {
             const int nm = 3 * p.n_mats, ns = 2 * p.sc.n_spheres;
-            for (int i = threadIdx.x; i < nm; i += blockDim.x) lds[2 * K + i] = p.sc.mats[i];
-            for (int i = threadIdx.x; i < ns; i += blockDim.x) lds[2 * K + nm + i] = p.sc.spheres[i];
-            S.mats = lds + 2 * K;
-            S.spheres = lds + 2 * K + nm;
+            for (int i = threadIdx.x; i < nm; i += blockDim.x) lds[KQ + i] = p.sc.mats[i];
+            for (int i = threadIdx.x; i < ns; i += blockDim.x) lds[KQ + nm + i] = p.sc.spheres[i];
+            S.mats = lds + KQ;
+            S.spheres = lds + KQ + nm;
         }
         __syncthreads();
-        S.np = K;
+        S.np = WIDE ? 0 : K;
+        S.wtop = WIDE ? K : 0;
         S.tp = 0;
     }
 #ifdef PT_PHASE_CLOCK
@@ -845,6 +941,9 @@ __global__ __launch_bounds__(NT, MINW) void k_render_sm(KParams p) {
     f3 rd = mk(0, 0, 0);
     float t = PT_FLAGS_IN_STATE ? -1.0f : 0.0f;
     int hprim = -1, bi = -1, leaf = 0;   // bi: walk position (WalkLinks); leaf: code of a hit leaf
+    // wide walk (lanes inside the guard): bi is its position (pt_wide.h), plus the stack and R
+    uint32_t we[kWideStack] = {0u, 0u};
+    int wR = -1;
 
 #ifdef PT_PHASE_CLOCK
     unsigned long long clk[6] = {0, 0, 0, 0, 0, 0};   // cycles + wave iterations per phase
@@ -1126,7 +1225,11 @@ __global__ __launch_bounds__(NT, MINW) void k_render_sm(KParams p) {
                                     (o.y >= p.root_box[2]) & (o.y <= p.root_box[3]) & (o.z >= p.root_box[4]) &
                                     (o.z <= p.root_box[5]);
                 const int img = (LDS && PT_FAST_SEG) ? oct_base(d, S.np << 5) : 0;   // octant image
-                bi = walk ? (inside ? root_skip : 0) + img : -1;
+                bi = walk ? ((WIDE && PT_FAST_SEG) ? 0 : (inside ? root_skip : 0) + img) : -1;
+                if (WIDE) {   // the wide walk starts at the root record with an empty stack
+                    we[0] = we[1] = 0u;
+                    wR = -1;
+                }
                 st = walk ? ST_TRAV : ST_SHADE;
             }
         } else if (nL > 0 && (nL >= p.leaf_thresh || low)) {
@@ -1140,6 +1243,11 @@ __global__ __launch_bounds__(NT, MINW) void k_render_sm(KParams p) {
                 const int code = LDS ? leaf : ~leaf;         // k << 2 | coplanar << 1 | single
                 s0 = (code >> 1) & ~1;                       // slots 2k, 2k+1
                 cop = (code & 2) != 0;
+                if (WIDE && fast) {                          // wide walk: bi = -2 - (g << 1 | cop)
+                    const int gc = -2 - bi;
+                    s0 = gc & ~1;                            // slots 2g, 2g+1
+                    cop = (gc & 1) != 0;
+                }
                 if (PT_WALK_SINKS && LDS && !COUNT && p.cons_walk) {   // sinks carry the pair k only
                     s0 = 2 * leaf;
                     cop = __float_as_int(tri_quad<LDS>(S, s0 + 1, 1).w) != 0;
@@ -1178,13 +1286,29 @@ __global__ __launch_bounds__(NT, MINW) void k_render_sm(KParams p) {
                     }
                 }
             }
+            if (WIDE) {
+                // the wide walk reached this leaf on the conservative test: as the culling walk,
+                // its own box is tested exactly at this t before a triangle may move t (leaf g's
+                // box at wlbox[2g], [2g + 1])
+                const bool chk = at & fast & (c1 | c2);
+                if (__any(chk)) {
+                    if (chk) {
+                        if (!slab_fast(S.wlbox[s0], S.wlbox[s0 + 1], o, d, rd, t)) c1 = c2 = false;
+                    }
+                }
+            }
             if (at) {
                 if (c1 | c2) {
                     t = c1 ? h1 : h2;
                     hprim = s0 + (c1 ? 0 : 1);
                 }
-                bi = cont;
-                st = bi > -1 ? ST_TRAV : ST_SHADE;
+                if (WIDE && fast) {   // the next pending child, or the resume position
+                    bi = ptw::wide_pop<kWideStack>(we, wR);
+                    st = bi >= 0 ? ST_TRAV : (bi == -1 ? ST_SHADE : ST_LEAF);
+                } else {
+                    bi = cont;
+                    st = bi > -1 ? ST_TRAV : ST_SHADE;
+                }
             }
         } else {
             // ---------------- TRAV: walk until a leaf is hit / the chain ends; yield to the
@@ -1198,6 +1322,12 @@ __global__ __launch_bounds__(NT, MINW) void k_render_sm(KParams p) {
                     trav_walk<true, COUNT, LDS, PADN, true>(S, o, d, rd, fast, t, live, mT, mL, mS, p.leaf_thresh, p.shade_thresh, p.trav_floor, st, bi, leaf, c);
                 else
                     trav_walk<false, COUNT, LDS, PADN, true>(S, o, d, rd, fast, t, live, mT, mL, mS, p.leaf_thresh, p.shade_thresh, p.trav_floor, st, bi, leaf, c);
+            } else if (WIDE) {
+                // lanes outside the guard walk the binary tree first (rare), then the wide walk
+                if (__ballot((st == ST_TRAV) & !fast))
+                    trav_walk<false, COUNT, LDS, PADN>(S, o, d, rd, fast, t, live, mT, mL, mS, p.leaf_thresh, p.shade_thresh, p.trav_floor, st, bi, leaf, c, !fast);
+                else
+                    trav_wide(S, o, rd, t, live, p.leaf_thresh, p.shade_thresh, p.trav_floor, st, bi, we, wR);
             } else if (all_fast) {
                 trav_walk<true, COUNT, LDS, PADN>(S, o, d, rd, fast, t, live, mT, mL, mS, p.leaf_thresh, p.shade_thresh, p.trav_floor, st, bi, leaf, c);
             } else {
@@ -1355,6 +1485,14 @@ struct pt_ctx {
     float4* d_walk_lds = nullptr;   // LDS walk image (DevScene)
     float4* d_walk_sk = nullptr;    // ... the culling walk's copy with its sink image
     size_t lds_bytes_sk = 0;
+    // the wide walk of global-memory scenes (pt_wide.h; nested trees inside the scene guard):
+    // records, exact leaf boxes, and the node / triangle arrays with leaf slots numbered by the
+    // wide tree's index (the binary walk of the lanes outside the guard shares them)
+    float4 *d_wrec = nullptr, *d_wlbox = nullptr, *d_nodesw = nullptr, *d_trisw = nullptr;
+    bool wide_ok = false;
+    int n_wide = 0;                 // wide index space (records + leaves)
+    float wide_cw[3] = {0, 0, 0};
+    int wide_off = 0;               // tuning key 16: 1 = the binary global walk
     unsigned long long* d_counters = nullptr;
     unsigned int* d_work = nullptr;
     int* d_frame = nullptr;                      // progressive graph frame counter
@@ -1453,7 +1591,11 @@ static void free_scene(pt_ctx* c) {
     (void)hipFree(c->d_nodes); (void)hipFree(c->d_tris); (void)hipFree(c->d_mats); (void)hipFree(c->d_spheres);
     (void)hipFree(c->d_walk_lds);
     (void)hipFree(c->d_walk_sk);
+    (void)hipFree(c->d_wrec); (void)hipFree(c->d_wlbox); (void)hipFree(c->d_nodesw); (void)hipFree(c->d_trisw);
     c->d_nodes = c->d_tris = c->d_mats = c->d_spheres = c->d_walk_lds = c->d_walk_sk = nullptr;
+    c->d_wrec = c->d_wlbox = c->d_nodesw = c->d_trisw = nullptr;
+    c->wide_ok = false;
+    c->n_wide = 0;
     c->scene_ok = false;
 }
 
@@ -1636,6 +1778,7 @@ int pt_upload_scene(pt_ctx* c, const float* tris, int n_tris, const float* bvh, 
     }
     std::vector<int> slot_of(n_nodes, -1);   // leaf slot by device node index
     std::vector<int> code_of(n_nodes, 0);    // leaf code by reference node index
+    std::vector<unsigned char> cop_of(n_nodes, 0);   // coplanar leaf pair, by reference node index
     // --- transpose to device layouts
     std::vector<float4> dt(8 * (size_t)std::max(n_leaves, 1));
     auto put_tri = [&](float4* q, int ti) {
@@ -1673,6 +1816,7 @@ int pt_upload_scene(pt_ctx* c, const float* tris, int n_tris, const float* bvh, 
             }
             a = ~((s << 2) | (cop ? 2 : 0) | (t0 == t1 ? 1 : 0));
             code_of[i] = ~a;
+            cop_of[i] = cop ? 1 : 0;
             b = (int)nd[11];
             slot_of[pos[i]] = s;
         } else {
@@ -1772,9 +1916,44 @@ int pt_upload_scene(pt_ctx* c, const float* tris, int n_tris, const float* bvh, 
             std::memcpy(&dt[8 * (size_t)leaf_slot[i] + 5].w, &cop, 4);
         }
     }
+    // The wide tree of the global-memory walk (pt_wide.h): nested trees only
+    // (the superset argument), built whatever the scene size -- variant 3 sends any scene to
+    // the global walk.  Its index g numbers records and leaves; leaf g's triangles go to slots
+    // 2g, 2g + 1 of a second triangle array and its exact box to wlbox[2g], and a second copy
+    // of the device nodes carries leaf codes g << 2 | coplanar << 1 | single for the binary
+    // walk of the lanes outside the guard.
+    ptw::WideTree wt;
+    std::vector<float4> dnw, dtw;
+    const bool wide = nested && ptw::wide_build(bvh, n_nodes, cop_of.data(), wt) == 0;
+    if (wide) {
+        dnw = dn;
+        dtw.assign(8 * (size_t)wt.n_index, make_float4(0, 0, 0, 0));
+        for (int i = 0; i < n_nodes; i++) {
+            const float* nd = bvh + 12 * (size_t)i;
+            if (!(nd[8] > -1.0f)) continue;
+            const int g = wt.g_of[i], t0 = (int)nd[8], t1 = (int)nd[9];
+            const int a = ~((g << 2) | (cop_of[i] ? 2 : 0) | (t0 == t1 ? 1 : 0));
+            std::memcpy(&dnw[2 * (size_t)pos[i] + 1].z, &a, 4);
+            put_tri(&dtw[8 * (size_t)g], t0);
+            put_tri(&dtw[8 * (size_t)g + 4], t1);
+        }
+    }
     HIPCHK(c, hipStreamSynchronize(c->stream));   // a render in flight may still read the old scene
     drop_graph(c);
     free_scene(c);
+    if (wide) {
+        const size_t nr = (size_t)wt.n_index;
+        HIPCHK(c, hipMalloc(&c->d_wrec, nr * 4 * sizeof(float4)));
+        HIPCHK(c, hipMalloc(&c->d_wlbox, nr * 2 * sizeof(float4)));
+        HIPCHK(c, hipMalloc(&c->d_nodesw, dnw.size() * sizeof(float4)));
+        HIPCHK(c, hipMalloc(&c->d_trisw, dtw.size() * sizeof(float4)));
+        HIPCHK(c, hipMemcpy(c->d_wrec, wt.rec.data(), nr * 4 * sizeof(float4), hipMemcpyHostToDevice));
+        HIPCHK(c, hipMemcpy(c->d_wlbox, wt.lbox.data(), nr * 2 * sizeof(float4), hipMemcpyHostToDevice));
+        HIPCHK(c, hipMemcpy(c->d_nodesw, dnw.data(), dnw.size() * sizeof(float4), hipMemcpyHostToDevice));
+        HIPCHK(c, hipMemcpy(c->d_trisw, dtw.data(), dtw.size() * sizeof(float4), hipMemcpyHostToDevice));
+        c->n_wide = wt.n_index;
+        std::memcpy(c->wide_cw, wt.cw, sizeof(c->wide_cw));
+    }
     if (nested) {
         HIPCHK(c, hipMalloc(&c->d_walk_sk, dsk.size() * sizeof(float4)));
         HIPCHK(c, hipMemcpy(c->d_walk_sk, dsk.data(), dsk.size() * sizeof(float4), hipMemcpyHostToDevice));
@@ -1808,6 +1987,7 @@ int pt_upload_scene(pt_ctx* c, const float* tris, int n_tris, const float* bvh, 
         if (!(nd[0] <= nd[4] && nd[1] <= nd[5] && nd[2] <= nd[6])) c->scene_fast = 0;
     }
     c->walk_nested = nested;
+    c->wide_ok = wide;
     c->order_sorted = false;      // the next sort pools the new scene's first short launches
     c->order_skip = 0;
     if (n_nodes > 0) {   // every box lies in the root box (nested): M_i bounds each |coordinate|
@@ -1900,6 +2080,12 @@ int pt_set_tuning(pt_ctx* c, int key, int value) {
     if (key == 15) {
         if (value != 0 && value != 1) return fail(c, PT_E_ARG, "culling walk: 0 = automatic, 1 = off");
         c->cons_off = value;
+        drop_graph(c);
+        return PT_OK;
+    }
+    if (key == 16) {
+        if (value != 0 && value != 1) return fail(c, PT_E_ARG, "wide global walk: 0 = automatic, 1 = off");
+        c->wide_off = value;
         drop_graph(c);
         return PT_OK;
     }
@@ -2039,8 +2225,16 @@ static int ensure_slot(pt_ctx* c, int sl, int n_frames) {
 }
 
 // Queue ids are 32-bit: a launch's items * 64 plus what the resident waves can reserve past
-// the end (each wave pulls at most 64 ids, twice after the queue ran dry) stay below 2^32.
-constexpr unsigned long long kIdLimit = (1ull << 32) - (1ull << 24);
+// the end stay below 2^32.  A wave reserves max(pull_batch, 64) ids per queue atomic and, once
+// the queue has run dry, at most two more reservations (the one that crossed the end and one
+// more; its lanes then finish), so the overshoot is at most (resident waves) * 2 *
+// max(pull_batch, 64), with at most persist_blocks * 4 resident waves (256-thread blocks) and
+// pull_batch at most 1024 (tuning key 4) or 256 (automatic).
+static unsigned long long id_limit(const pt_ctx* c) {
+    const unsigned long long pb = (unsigned long long)std::max(256, c->pull_batch);
+    const unsigned long long slack = (unsigned long long)c->persist_blocks * 4ull * 2ull * pb;
+    return (1ull << 32) - slack - (1ull << 20);
+}
 
 // Frames of one launch for a render of n_frames: the largest count whose frame-split scratch
 // (12 B per pixel-frame) fits the context's budget and whose queue ids stay 32-bit.  A longer
@@ -2057,8 +2251,9 @@ static int launch_frames(const pt_ctx* c, int n_frames) {
         // strictly decreases to at most 1: the loop ends)
         const unsigned long long by_budget = std::max(1ull, c->scratch_budget / (px * 12ull));
         const unsigned long long ng = (unsigned long long)((n + g - 1) / g);
-        const unsigned long long by_ids = (kIdLimit / tiles64) * (unsigned long long)g;
-        if (((unsigned long long)n <= by_budget && ng * tiles64 < kIdLimit) || n == 1) return n;
+        const unsigned long long lim = id_limit(c);
+        const unsigned long long by_ids = (lim / tiles64) * (unsigned long long)g;
+        if (((unsigned long long)n <= by_budget && ng * tiles64 < lim) || n == 1) return n;
         const unsigned long long m = std::min<unsigned long long>({(unsigned long long)n - 1, by_budget, by_ids});
         n = (int)std::max<unsigned long long>(m, 1ull);
     }
@@ -2075,6 +2270,15 @@ static bool cons_walk_on(const pt_ctx* c) {
     const size_t mw = (size_t)(c->minw ? c->minw : 7);
     const auto blocks = [mw](size_t b) { return b ? std::min(mw, (size_t)(160 * 1024) / b) : mw; };
     return blocks(c->lds_bytes_sk) >= blocks(c->lds_bytes);
+}
+
+// Whether a global-memory launch walks the wide tree: the scene has one
+// (a nested tree), it lies inside the scene half of the exact-reciprocal guard (otherwise no
+// lane could use it), tuning key 16 leaves it on, nothing is counted, and the occupancy is
+// the automatic 6 waves per SIMD (the wide instantiations').
+constexpr int kWideTop = 512;   // wide records staged in LDS (24 KiB per 256-thread block)
+static bool wide_walk_on(const pt_ctx* c) {
+    return c->wide_ok && c->scene_fast && !c->wide_off && !c->counting && (c->minw == 0 || c->minw == 6);
 }
 
 // Threads per workgroup of the state-machine kernel on an LDS-staged scene of `lds` bytes:
@@ -2214,6 +2418,17 @@ static int enqueue_render(pt_ctx* c, int frame_first, int n_frames, int acc_firs
     // variants: 0 state machine (default), 3 = 0 with the scene forced to stay in global memory
     const int variant = c->variant;
     const bool use_lds = variant == 0 && lds_staged(c);
+    // the global-memory walk of a nested tree takes the wide tree (pt_wide.h) unless tuning
+    // key 16 turns it off; counting builds keep the binary walk (their counts are the
+    // reference's), and so do occupancy overrides other than 6 waves per SIMD
+    const bool use_wide = !use_lds && wide_walk_on(c);
+    if (use_wide) {
+        p.sc.nodes = c->d_nodesw;
+        p.sc.tris = c->d_trisw;
+        p.sc.wrec = c->d_wrec;
+        p.sc.wlbox = c->d_wlbox;
+        std::memcpy(p.wide_cw, c->wide_cw, sizeof(p.wide_cw));
+    }
     if (overlap) {
         if (c->adone_rec[sl]) HIPCHK(c, hipStreamWaitEvent(rs, c->ev_adone[sl], 0));
         if (c->fence_rec) HIPCHK(c, hipStreamWaitEvent(rs, c->ev_fence, 0));
@@ -2243,7 +2458,11 @@ static int enqueue_render(pt_ctx* c, int frame_first, int n_frames, int acc_firs
         // materials + spheres beside the top nodes when they are small (<= 4 KiB)
         const size_t shade_bytes = (size_t)(3 * c->n_mats + 2 * c->n_spheres) * sizeof(float4);
         p.shade_lds = shade_bytes <= 4096;
-        const size_t top_lds = (size_t)p.n_top * 2 * sizeof(float4) + (p.shade_lds ? shade_bytes : 0);
+        if (use_wide)   // top records: 48 B each, within what mw blocks per CU leave beside the shading records
+            p.wide_top = (int)std::min<size_t>({(size_t)c->n_wide, (size_t)kWideTop,
+                                                ((size_t)160 * 1024 / (size_t)mw - (p.shade_lds ? shade_bytes : 0) - 256) / 48});
+        const size_t top_lds = use_wide ? (size_t)p.wide_top * 3 * sizeof(float4) + (p.shade_lds ? shade_bytes : 0)
+                                        : (size_t)p.n_top * 2 * sizeof(float4) + (p.shade_lds ? shade_bytes : 0);
 #define PT_LAUNCH_SM(L, M)                                                                                \
     if (c->counting && p.rgb) hipLaunchKernelGGL((k_render_sm<true, L, 5, M, true>), grid, dim3(256), L ? lds : top_lds, rs, p); \
     else if (c->counting) hipLaunchKernelGGL((k_render_sm<true, L, 5, M, false>), grid, dim3(256), L ? lds : top_lds, rs, p); \
@@ -2259,7 +2478,12 @@ static int enqueue_render(pt_ctx* c, int frame_first, int n_frames, int acc_firs
     else hipLaunchKernelGGL((k_render_sm<false, true, MW, false, false, false, NT>), grid, dim3(NT), lds, rs, p);
         // lds_threads: LDS scene, variant 0, one ray per pixel; the register budget of the
         // waves that are resident (6, 6, 4 per SIMD), not of 7
-        if (nt > 256) {
+        if (use_wide) {
+            if (p.rgb && p.rpp > 1) hipLaunchKernelGGL((k_render_sm<false, false, 6, true, true, false, 256, true>), grid, dim3(256), top_lds, rs, p);
+            else if (p.rgb) hipLaunchKernelGGL((k_render_sm<false, false, 6, false, true, false, 256, true>), grid, dim3(256), top_lds, rs, p);
+            else if (p.rpp > 1) hipLaunchKernelGGL((k_render_sm<false, false, 6, true, false, false, 256, true>), grid, dim3(256), top_lds, rs, p);
+            else hipLaunchKernelGGL((k_render_sm<false, false, 6, false, false, false, 256, true>), grid, dim3(256), top_lds, rs, p);
+        } else if (nt > 256) {
             if (nt == 512) { PT_LAUNCH_WIDE(512, 6) }
             else if (nt == 768) { PT_LAUNCH_WIDE(768, 6) }
             else { PT_LAUNCH_WIDE(1024, 4) }
@@ -2491,8 +2715,8 @@ int pt_get_config(const pt_ctx* c, pt_config* out) {
 // buffers of the same sizes, contents undefined -- and returns both contexts' buffer pointers
 // and sizes, so the caller can fill dst's from src's (an RCCL broadcast across devices or a
 // device copy).  Both contexts must have the same width (tile facts are per image).
-int pt__scene_replicate_layout(pt_ctx* dst, const pt_ctx* src, void* dptr[6], const void* sptr[6],
-                               size_t bytes[6]) {
+int pt__scene_replicate_layout(pt_ctx* dst, const pt_ctx* src, void* dptr[10], const void* sptr[10],
+                               size_t bytes[10]) {
     if (!dst || !src || !dptr || !sptr || !bytes) return PT_E_ARG;
     if (!src->scene_ok) return fail(dst, PT_E_STATE, "source context has no scene");
     HIPCHK(dst, hipSetDevice(dst->cfg.device));
@@ -2502,10 +2726,13 @@ int pt__scene_replicate_layout(pt_ctx* dst, const pt_ctx* src, void* dptr[6], co
     const size_t nd = 2 * (size_t)std::max(src->n_nodes, 1), nt = 8 * (size_t)std::max(src->n_slots / 2, 1);
     const size_t nm = 3 * (size_t)std::max(src->n_mats, 1), ns = 2 * (size_t)std::max(src->n_spheres, 1);
     const size_t nw = 16 * (size_t)src->walk_np, nk = src->d_walk_sk ? 18 * (size_t)src->walk_np : 0;
-    const size_t sz[6] = {nd, nt, nm, ns, nw, nk};
-    float4** mine[6] = {&dst->d_nodes, &dst->d_tris, &dst->d_mats, &dst->d_spheres, &dst->d_walk_lds, &dst->d_walk_sk};
-    const float4* theirs[6] = {src->d_nodes, src->d_tris, src->d_mats, src->d_spheres, src->d_walk_lds, src->d_walk_sk};
-    for (int i = 0; i < 6; i++) {
+    const size_t ni = src->wide_ok ? (size_t)src->n_wide : 0;   // the wide walk's arrays (pt_wide.h)
+    const size_t sz[10] = {nd, nt, nm, ns, nw, nk, 4 * ni, 2 * ni, ni ? nd : 0, 8 * ni};
+    float4** mine[10] = {&dst->d_nodes, &dst->d_tris, &dst->d_mats, &dst->d_spheres, &dst->d_walk_lds, &dst->d_walk_sk,
+                         &dst->d_wrec, &dst->d_wlbox, &dst->d_nodesw, &dst->d_trisw};
+    const float4* theirs[10] = {src->d_nodes, src->d_tris, src->d_mats, src->d_spheres, src->d_walk_lds, src->d_walk_sk,
+                                src->d_wrec, src->d_wlbox, src->d_nodesw, src->d_trisw};
+    for (int i = 0; i < 10; i++) {
         bytes[i] = sz[i] * sizeof(float4);
         sptr[i] = theirs[i];
         if (sz[i]) HIPCHK(dst, hipMalloc(mine[i], bytes[i]));
@@ -2519,6 +2746,9 @@ int pt__scene_replicate_layout(pt_ctx* dst, const pt_ctx* src, void* dptr[6], co
     dst->scene_fast = src->scene_fast;
     dst->walk_nested = src->walk_nested;
     std::memcpy(dst->cons_m, src->cons_m, sizeof(dst->cons_m));
+    dst->wide_ok = src->wide_ok;
+    dst->n_wide = src->n_wide;
+    std::memcpy(dst->wide_cw, src->wide_cw, sizeof(dst->wide_cw));
     dst->walk_np = src->walk_np;
     dst->lds_bytes = src->lds_bytes;
     dst->lds_bytes_sk = src->lds_bytes_sk;
@@ -2526,7 +2756,15 @@ int pt__scene_replicate_layout(pt_ctx* dst, const pt_ctx* src, void* dptr[6], co
     dst->root_child = src->root_child;
     dst->order_sorted = false;
     dst->order_skip = 0;
-    dst->scene_ok = true;
+    // scene_ok stays false until the caller has filled the buffers (pt__scene_set_ready): a
+    // failed broadcast or copy must not leave a context rendering from uninitialised memory
+    dst->scene_ok = false;
+    return PT_OK;
+}
+
+int pt__scene_set_ready(pt_ctx* c, int ready) {
+    if (!c) return PT_E_ARG;
+    c->scene_ok = ready != 0 && c->d_mats != nullptr;
     return PT_OK;
 }
 

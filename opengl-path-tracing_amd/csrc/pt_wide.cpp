@@ -1,0 +1,214 @@
+// pt_wide.cpp -- host builder of the 4-wide quantised tree of the global-memory walk
+// (pt_wide.h).  Input: the reference's threaded binary tree (bvh.h:173-268
+// builds it; computeShader.c:389-431 walks it), which must be nested (pt_bvh_culling_ok).
+#include "pt_wide.h"
+
+#include <algorithm>
+#include <array>
+#include <cmath>
+#include <cstring>
+
+namespace ptw {
+namespace {
+
+struct BN {
+    float lo[3], hi[3];
+    int left = -1, right = -1;
+    bool leaf = false;
+};
+
+// Sign of (O + q 2^e) - b, exactly: q 2^e is exact in binary64 and TwoSum gives the rounding
+// error of the sum, so the comparison with the binary32 b is exact (no overflow here).
+int cmp_plane(float O, int q, int e, float b) {
+    const double a = (double)O, c = std::ldexp((double)q, e);
+    const double s = a + c, bb = s - a;
+    const double err = (a - (s - bb)) + (c - bb);
+    const double B = (double)b;
+    if (s < B) return -1;
+    if (s > B) return 1;
+    return err < 0.0 ? -1 : (err > 0.0 ? 1 : 0);
+}
+
+// Smallest e in [-100, 100] with L + 255 * 2^e >= H (the codes of a record's axis then span
+// its box).
+int axis_exp(float L, float H) {
+    const double ext = (double)H - (double)L;
+    int e = -100;
+    if (ext > 0.0) e = std::max(-100, (int)std::ceil(std::log2(ext / 255.0)));
+    while (e < 100 && cmp_plane(L, 255, e, H) < 0) e++;
+    while (e > -100 && cmp_plane(L, 255, e - 1, H) >= 0) e--;
+    return e;
+}
+
+// Outward codes of the child interval [cl, ch] on an axis with origin L and step 2^e:
+// the largest q with L + q 2^e <= cl, the smallest with L + q 2^e >= ch.
+void codes(float L, int e, float cl, float ch, int& qlo, int& qhi) {
+    const double st = std::ldexp(1.0, e);
+    qlo = (int)std::floor(((double)cl - (double)L) / st);
+    qlo = std::min(255, std::max(0, qlo));
+    while (qlo > 0 && cmp_plane(L, qlo, e, cl) > 0) qlo--;
+    while (qlo < 255 && cmp_plane(L, qlo + 1, e, cl) <= 0) qlo++;
+    qhi = (int)std::ceil(((double)ch - (double)L) / st);
+    qhi = std::min(255, std::max(0, qhi));
+    while (qhi < 255 && cmp_plane(L, qhi, e, ch) < 0) qhi++;
+    while (qhi > 0 && cmp_plane(L, qhi - 1, e, ch) >= 0) qhi--;
+}
+
+double area(const BN& b) {
+    const double dx = (double)b.hi[0] - b.lo[0], dy = (double)b.hi[1] - b.lo[1], dz = (double)b.hi[2] - b.lo[2];
+    return dx * dy + dy * dz + dz * dx;
+}
+
+int link_of(float v, int n) {
+    if (!(v >= -1.0f && v < (float)n) || v != (float)(int)v) return -2;
+    return (int)v;
+}
+
+float round_up_f(double v) {
+    float f = (float)v;
+    if ((double)f < v) f = std::nextafter(f, INFINITY);
+    return f;
+}
+
+}  // namespace
+
+int wide_build(const float* bvh, int n_nodes, const unsigned char* leaf_cop, WideTree& out) {
+    out = WideTree();
+    if (n_nodes <= 0) return -1;
+    std::vector<BN> bn(n_nodes);
+    for (int i = 0; i < n_nodes; i++) {
+        const float* nd = bvh + 12 * (size_t)i;
+        for (int q = 0; q < 3; q++) { bn[i].lo[q] = nd[q]; bn[i].hi[q] = nd[4 + q]; }
+        bn[i].leaf = nd[8] > -1.0f;
+    }
+    // children of the internal nodes reachable from the root (the threading of a nested tree:
+    // hit link = left child, the left child's miss link = the right child)
+    {
+        std::vector<int> st{0};
+        std::vector<unsigned char> seen(n_nodes, 0);
+        while (!st.empty()) {
+            const int x = st.back();
+            st.pop_back();
+            if (x < 0 || x >= n_nodes || seen[x]) return -1;
+            seen[x] = 1;
+            if (bn[x].leaf) continue;
+            const int l = link_of(bvh[12 * (size_t)x + 10], n_nodes);
+            if (l < 0) return -1;
+            const int r = link_of(bvh[12 * (size_t)l + 11], n_nodes);
+            if (r < 0) return -1;
+            bn[x].left = l;
+            bn[x].right = r;
+            st.push_back(r);
+            st.push_back(l);
+        }
+    }
+    // record frontiers: [left, right], then the internal member of largest surface area
+    // replaced by its two children (in place: the list stays in preorder) until 4 members
+    auto frontier = [&](int x, int* f) {
+        if (bn[x].leaf) { f[0] = x; return 1; }   // a root leaf: a record with that one child
+        int n = 2;
+        f[0] = bn[x].left;
+        f[1] = bn[x].right;
+        while (n < 4) {
+            int best = -1;
+            double ba = -1.0;
+            for (int k = 0; k < n; k++)
+                if (!bn[f[k]].leaf && area(bn[f[k]]) > ba) { ba = area(bn[f[k]]); best = k; }
+            if (best < 0) break;
+            const int y = f[best];
+            for (int k = n; k > best + 1; k--) f[k] = f[k - 1];
+            f[best] = bn[y].left;
+            f[best + 1] = bn[y].right;
+            n++;
+        }
+        return n;
+    };
+    // breadth-first numbering: a record's children take consecutive indices (cbase + j)
+    out.g_of.assign(n_nodes, -1);
+    std::vector<int> recs{0}, rdepth{0};          // binary node of each record, in g order
+    std::vector<int> parent_g{-1}, parent_slot{0};
+    std::vector<int> g_of_rec;                     // record position -> g
+    std::vector<std::array<int, 4>> kids;
+    std::vector<int> nkids;
+    out.g_of[0] = 0;
+    int next = 1;
+    g_of_rec.push_back(0);
+    for (size_t qi = 0; qi < recs.size(); qi++) {
+        int f[4];
+        const int n = frontier(recs[qi], f);
+        std::array<int, 4> k = {-1, -1, -1, -1};
+        for (int j = 0; j < n; j++) {
+            k[j] = f[j];
+            if (next >= kMaxRecords) return -1;
+            out.g_of[f[j]] = next++;
+            if (!bn[f[j]].leaf) {
+                recs.push_back(f[j]);
+                rdepth.push_back(rdepth[qi] + 1);
+                parent_g.push_back(g_of_rec[qi]);
+                parent_slot.push_back(j);
+                g_of_rec.push_back(out.g_of[f[j]]);
+            }
+        }
+        kids.push_back(k);
+        nkids.push_back(n);
+    }
+    out.n_index = next;
+    out.bn_of.assign(next, -1);
+    for (int i = 0; i < n_nodes; i++)
+        if (out.g_of[i] >= 0) out.bn_of[out.g_of[i]] = i;
+    out.bn_of[0] = 0;
+    out.n_records = (int)recs.size();
+    out.depth = 0;
+    for (int d : rdepth) out.depth = std::max(out.depth, d + 1);
+    out.rec.assign((size_t)next * 16, 0.0f);
+    out.lbox.assign((size_t)next * 8, 0.0f);
+    std::vector<int> exit_of(next, -1), pos_of(next, -1);
+    for (size_t qi = 0; qi < recs.size(); qi++) pos_of[g_of_rec[qi]] = (int)qi;
+    for (size_t qi = 0; qi < recs.size(); qi++) {
+        const int x = recs[qi], g = g_of_rec[qi];
+        const int n = nkids[qi];
+        if (qi > 0) {   // resume the parent after this slot; after its last slot, the parent's exit
+            const int pg = parent_g[qi], ps = parent_slot[qi];
+            exit_of[g] = ps + 1 < nkids[pos_of[pg]] ? ((pg << 3) | (ps + 1)) : exit_of[pg];
+        }
+        float* r = &out.rec[(size_t)g * 16];
+        int e[3];
+        for (int i = 0; i < 3; i++) e[i] = axis_exp(bn[x].lo[i], bn[x].hi[i]);
+        uint32_t lo_w[3] = {0, 0, 0}, hi_w[3] = {0, 0, 0}, types = 0;
+        for (int j = 0; j < n; j++) {
+            const BN& c = bn[kids[qi][j]];
+            for (int i = 0; i < 3; i++) {
+                int ql, qh;
+                codes(bn[x].lo[i], e[i], c.lo[i], c.hi[i], ql, qh);
+                lo_w[i] |= (uint32_t)ql << (8 * j);
+                hi_w[i] |= (uint32_t)qh << (8 * j);
+            }
+            const uint32_t ty = c.leaf ? (2u | (leaf_cop && leaf_cop[kids[qi][j]] ? 1u : 0u)) : 1u;
+            types |= ty << (2 * j);
+        }
+        const uint32_t w = ((uint32_t)(e[0] & 0xff)) | ((uint32_t)(e[1] & 0xff) << 8) |
+                           ((uint32_t)(e[2] & 0xff) << 16) | (types << 24);
+        const int cbase = out.g_of[kids[qi][0]];
+        const uint32_t u[12] = {0, 0, 0, w, lo_w[0], hi_w[0], lo_w[1], hi_w[1], lo_w[2], hi_w[2],
+                                (uint32_t)cbase, (uint32_t)exit_of[g]};
+        std::memcpy(r, u, sizeof(u));
+        r[0] = bn[x].lo[0];
+        r[1] = bn[x].lo[1];
+        r[2] = bn[x].lo[2];
+        for (int j = 0; j < n; j++) {
+            const int c = kids[qi][j];
+            if (!bn[c].leaf) continue;
+            float* b = &out.lbox[(size_t)out.g_of[c] * 8];
+            b[0] = bn[c].lo[0]; b[1] = bn[c].hi[0]; b[2] = bn[c].lo[1]; b[3] = bn[c].hi[1];
+            b[4] = bn[c].lo[2]; b[5] = bn[c].hi[2];
+            out.n_leaves++;
+        }
+    }
+    for (int q = 0; q < 3; q++) {
+        const double m = std::max(std::fabs((double)bn[0].lo[q]), std::fabs((double)bn[0].hi[q]));
+        out.cw[q] = round_up_f(std::ldexp(m, -18));
+    }
+    return 0;
+}
+
+}  // namespace ptw
