@@ -19,6 +19,7 @@ N>1:   python -m torch.distributed.run --nproc-per-node N bench.py --gpus N ...
 from __future__ import annotations
 
 import argparse
+import hashlib
 import json
 import os
 import sys
@@ -75,6 +76,27 @@ def cpu_model():
     return "unknown"
 
 
+def pmc_for(traffic_json, lib_path, W, H, chunk, scene, world):
+    """-> (PMC summary or None, why not, sha256 of the library).  The PMC figures count only
+    for this exact build and workload: the pass records the sha256 of the library it
+    profiled (tools/pmc_traffic.py), and a rebuilt kernel without a fresh pass gets frac =
+    null -- dividing an old instruction count by a new time would not be a roofline."""
+    with open(lib_path, "rb") as fh:
+        lib_sha = hashlib.sha256(fh.read()).hexdigest()
+    try:
+        with open(traffic_json) as fh:
+            tj = json.load(fh)
+    except (OSError, ValueError) as e:
+        return None, "no PMC pass (%s)" % e, lib_sha
+    if (tj.get("width"), tj.get("height"), tj.get("chunk"), tj.get("scene")) != (W, H, chunk, scene) or world != 1:
+        return None, "PMC pass is of another workload (%s %sx%s, %s frames per launch)" % (
+            tj.get("scene"), tj.get("width"), tj.get("height"), tj.get("chunk")), lib_sha
+    if tj.get("lib_sha256") != lib_sha:
+        return None, "PMC pass profiled another build (lib sha256 %s, this build %s)" % (
+            str(tj.get("lib_sha256"))[:12], lib_sha[:12]), lib_sha
+    return tj, None, lib_sha
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -94,6 +116,8 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="nccl = RCCL over xGMI (default); gloo = CPU rehearsal of the N>1 path")
+    ap.add_argument("--dump-frame", default=None,
+                    help="rank 0 saves the last step's assembled RGBA32F frame here (np.save; tests)")
     ap.add_argument("--traffic-json", default=os.path.join(REPO, "profiles", "traffic_latest.json"),
                     help="PMC-derived HBM bytes per launch (tools/pmc_traffic.py)")
     args = ap.parse_args()
@@ -183,6 +207,9 @@ def main():
         rmax = pt_dist.rows_max(H, world)
         dev = "cuda" if args.dist_backend == "nccl" else "cpu"
         send = torch.zeros((rmax, W, 4), dtype=torch.float32, device=dev)
+        # the rows leave the render context by a device copy in both modes (the RCCL path's
+        # pt_copy_rows_device); the gloo rehearsal then stages them through host memory
+        dsend = send if dev == "cuda" else torch.zeros((rmax, W, 4), dtype=torch.float32, device="cuda")
 
     def step():
         if use_graph:
@@ -193,10 +220,9 @@ def main():
                 pt.render_async(f0, n, 0 if f0 == 1 else 1)
         pt.sync()
         if distributed:
-            if args.dist_backend == "nccl":
-                pt.copy_rows_device(send.data_ptr(), pt.rows_local * W * 16)
-            else:
-                send[: pt.rows_local] = torch.from_numpy(pt.read_rgba32f())
+            pt.copy_rows_device(dsend.data_ptr(), pt.rows_local * W * 16)
+            if args.dist_backend != "nccl":
+                send.copy_(dsend)
             img = pt_dist.gather_image(send, H, world)
             if args.dist_backend == "nccl":
                 torch.cuda.synchronize()
@@ -210,7 +236,7 @@ def main():
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        step()
+        img = step()
     torch.cuda.synchronize()
     barrier()
     dt = time.perf_counter() - t0
@@ -254,19 +280,14 @@ def main():
     #   achieved = SQ_INSTS_VALU per launch / the live launch time (HIP events, this run)
     #   peak     = 1024 SIMDs x held clock / 2 cycles per wave64 VALU instruction
     #   busy_frac_pmc = SQ_INSTS_VALU x 2 / (1024 x GRBM_GUI_ACTIVE / 8), all from the PMC pass
-    pmc = None
-    try:
-        with open(args.traffic_json) as fh:
-            tj = json.load(fh)
-        if (tj.get("width"), tj.get("height"), tj.get("chunk"), tj.get("scene")) == (W, H, chunk, scene) \
-                and world == 1:
-            pmc = tj
-    except (OSError, ValueError):
-        pass
+    pmc, stale, lib_sha = pmc_for(args.traffic_json, pt_host.LIB_PATH, W, H, chunk, scene, world)
     hbm = {"algorithmic_gbs": round(achieved, 1), "algorithmic_frac": round(achieved / HBM_PEAK_GBS, 4),
            "algorithmic_bytes_per_launch": int(bytes_per_launch), "peak": HBM_PEAK_GBS, "unit": "GB/s"}
     roofline = {"bound": "valu", "achieved": None, "peak": None, "unit": "G wave-VALU instr/s", "frac": None,
-                "traffic": None, "avg_launch_ms": round(avg_launch_ms, 3), "n_launches": n_launch}
+                "traffic": None, "avg_launch_ms": round(avg_launch_ms, 3), "n_launches": n_launch,
+                "lib_sha256": lib_sha[:16]}
+    if stale:
+        roofline["pmc_stale"] = stale
     if pmc is not None and pmc.get("valu_instr_per_launch"):
         cnt = pmc["counters_per_launch"]
         vi = pmc["valu_instr_per_launch"]
@@ -285,6 +306,8 @@ def main():
                        measured_frac=round(tb / (avg_launch_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
                        traffic_over_algorithmic=round(tb / bytes_per_launch, 2))
         roofline["source"] = pmc.get("source", "profiles/traffic_latest.json")
+        if pmc.get("pmc_launch_ms"):   # the PMC pass's own launch time beside the live one
+            roofline["pmc_launch_ms"] = round(pmc["pmc_launch_ms"], 3)
     roofline["hbm"] = hbm
     roofline["basis"] = ("VALU issue: achieved = PMC SQ_INSTS_VALU per launch / live avg launch time (HIP events on "
                          "the render stream); peak = 1024 SIMDs x PMC-held clock / 2; HBM kept as a secondary "
@@ -308,6 +331,9 @@ def main():
                          "%.2f s); ms/frame = %.1f" % (threads, W, H, args.cpu_spp, int(ccnt[0]), cdt,
                                                         cdt * 1e3 / args.cpu_spp)}
 
+    if args.dump_frame and rank == 0:
+        import numpy as np
+        np.save(args.dump_frame, img.cpu().numpy() if img is not None else pt.read_rgba32f())
     if rank == 0:
         line = {
             "metric": METRIC, "value": round(value, 3), "unit": "Mrays/s", "n_gpus": world,

@@ -747,7 +747,10 @@ __device__ __forceinline__ void trav_walk(const SceneView& S, f3 o, f3 d, f3 rd,
 // position.  Lanes inside the exact-reciprocal guard only; their leaf boxes are re-tested
 // exactly in the leaf phase before a triangle may move t.  The first `wtop` records sit in
 // LDS as three planes (q0 at [i], q1 at [wtop + i], q2 at [2 wtop + i]).
-constexpr int kWideStack = 2;
+#ifndef PT_WIDE_STACK
+#define PT_WIDE_STACK 2
+#endif
+constexpr int kWideStack = PT_WIDE_STACK;
 #ifndef PT_WIDE_UNROLL
 #define PT_WIDE_UNROLL 2
 #endif
@@ -942,7 +945,7 @@ __global__ __launch_bounds__(NT, MINW) void k_render_sm(KParams p) {
     float t = PT_FLAGS_IN_STATE ? -1.0f : 0.0f;
     int hprim = -1, bi = -1, leaf = 0;   // bi: walk position (WalkLinks); leaf: code of a hit leaf
     // wide walk (lanes inside the guard): bi is its position (pt_wide.h), plus the stack and R
-    uint32_t we[kWideStack] = {0u, 0u};
+    uint32_t we[kWideStack] = {};
     int wR = -1;
 
 #ifdef PT_PHASE_CLOCK
@@ -1227,7 +1230,8 @@ __global__ __launch_bounds__(NT, MINW) void k_render_sm(KParams p) {
                 const int img = (LDS && PT_FAST_SEG) ? oct_base(d, S.np << 5) : 0;   // octant image
                 bi = walk ? ((WIDE && PT_FAST_SEG) ? 0 : (inside ? root_skip : 0) + img) : -1;
                 if (WIDE) {   // the wide walk starts at the root record with an empty stack
-                    we[0] = we[1] = 0u;
+#pragma unroll
+                    for (int k = 0; k < kWideStack; k++) we[k] = 0u;
                     wR = -1;
                 }
                 st = walk ? ST_TRAV : ST_SHADE;

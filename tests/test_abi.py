@@ -71,3 +71,26 @@ def test_create_without_gpu_fails_loudly():
     with pytest.raises(H.PTError) as e:
         H.PathTracer(32, 32)
     assert e.value.code == -5
+
+
+def test_bench_roofline_needs_the_profiled_build(tmp_path):
+    """bench.py's VALU roofline uses a PMC pass only for the exact library it profiled
+    (sha256) and the same workload; otherwise frac is null with the reason."""
+    import hashlib
+    import json
+    import bench
+    lib = tmp_path / "libptrace.so"
+    lib.write_bytes(b"build A")
+    tj = tmp_path / "traffic.json"
+    meta = dict(scene="cornell", width=1920, height=1080, chunk=1024, valu_instr_per_launch=1.0)
+    tj.write_text(json.dumps(dict(meta, lib_sha256=hashlib.sha256(b"build A").hexdigest())))
+    pmc, stale, sha = bench.pmc_for(str(tj), str(lib), 1920, 1080, 1024, "cornell", 1)
+    assert pmc is not None and stale is None and sha == hashlib.sha256(b"build A").hexdigest()
+    lib.write_bytes(b"build B")                  # rebuilt kernel, no fresh PMC pass
+    pmc, stale, _ = bench.pmc_for(str(tj), str(lib), 1920, 1080, 1024, "cornell", 1)
+    assert pmc is None and "another build" in stale
+    lib.write_bytes(b"build A")
+    pmc, stale, _ = bench.pmc_for(str(tj), str(lib), 1920, 1080, 128, "cornell", 1)   # other launch shape
+    assert pmc is None and "another workload" in stale
+    pmc, stale, _ = bench.pmc_for(str(tmp_path / "missing.json"), str(lib), 1920, 1080, 1024, "cornell", 1)
+    assert pmc is None and "no PMC pass" in stale

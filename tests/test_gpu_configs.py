@@ -153,3 +153,34 @@ def test_reference_scenes_full_hd_sampled(ref_scenes, name):
     assert_bitwise(img, want_img, "%s counting build" % name)
     assert [cnt["segments"], cnt["node_visits"], cnt["tri_tests"], cnt["sphere_tests"], cnt["hits"]] == \
         [int(x) for x in want_cnt]
+
+
+def test_c5_graph_frame_range_strip(cornell_scene):
+    """The C5 frame range through the captured graph: a 3840-wide strip of the 4K frame
+    (rows 0, 135, ..., rank 0 of a 135-way row split: the full-width camera rays) replayed
+    from pt_progressive_reset(2980) across frame 2986, where frame * 719393 passes 2^31
+    (computeShader.c:514-515: the seed wraps mod 2^32), then from 4090 across 4096, on top of
+    the first replay's image (the running mean :548-551 at float(frame) ~ 4096).  Sampled
+    pixels span every x, including x >= 2325, where the x term alone passes 2^31."""
+    W, Hh, world = 3840, 2160, 135
+    pt = H.PathTracer(W, Hh, max_bounce=8, rank=0, world=world)
+    pt.upload(cornell_scene)
+    pt.progressive_setup(frames_per_launch=4, launches_per_replay=2)
+    pt.progressive_reset(2980)
+    pt.progressive_run(replays=1)                  # frames 2980..2987, accumulate from frame 2980
+    a = pt.read_rgba32f()
+    pt.progressive_reset(4090)
+    pt.progressive_run(replays=1)                  # frames 4090..4097
+    b = pt.read_rgba32f()
+    pt.close()
+    rows = np.arange(0, Hh, world)
+    assert a.shape == (len(rows), W, 4)
+    rng = np.random.default_rng(57)
+    li = np.concatenate([rng.integers(0, len(rows), 3000), np.zeros(W, int), np.full(W, len(rows) - 1)])
+    xs = np.concatenate([rng.integers(0, W, 3000), np.arange(W), np.arange(W)])
+    ys = rows[li]
+    wa = O.render_pixels(cornell_scene, W, Hh, xs, ys, max_bounce=8, frame_first=2980, n_frames=8, acc_first=1)
+    assert_bitwise(a[li, xs], wa, "graph frames 2980..2987")
+    wb = O.render_pixels(cornell_scene, W, Hh, xs, ys, max_bounce=8, frame_first=4090, n_frames=8, acc_first=1,
+                         prior=wa)
+    assert_bitwise(b[li, xs], wb, "graph frames 4090..4097")

@@ -1,0 +1,52 @@
+"""bench.py's N>1 path with the HIP kernels: two ranks on device 0 over
+gloo run the bench's own pt_dist.broadcast_scene -> pt_copy_rows_device -> pt_dist.gather_image
+path; rank 0's assembled frame must equal one context's render bit for bit (each pixel's RNG
+stream depends only on (x, y, frame), computeShader.c:514-515).  RCCL cannot put two ranks on
+one GPU, so the 8-GPU RCCL run stays the driver's; tests/test_dist.py checks the gather on CPU.
+"""
+import os
+import socket
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+import pt_host as H
+from test_gpu_parity import assert_bitwise
+
+pytestmark = pytest.mark.gpu
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+@pytest.mark.parametrize("world,config", [(2, "C2"), (3, "C3")])
+def test_bench_ranks_gloo_one_gpu(tmp_path, cornell_scene, world, config):
+    W, Hh, spp, chunk = 160, 90, 6, 3
+    out = str(tmp_path / "frame.npy")
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0", MASTER_ADDR="127.0.0.1")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(world),
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), "bench.py", "--gpus", str(world),
+           "--config", config, "--dist-backend", "gloo", "--width", str(W), "--height", str(Hh), "--spp", str(spp),
+           "--chunk", str(chunk), "--steps", "1", "--warmup", "1", "--no-cold", "--no-cpu-baseline",
+           "--dump-frame", out]
+    r = subprocess.run(cmd, cwd=REPO, env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
+    img = np.load(out)
+    import pt_scenes
+    sc = cornell_scene if config == "C2" else H.setupBuffers(*pt_scenes.write_scene("bunny", os.path.join(REPO, "scenes")))
+    pt = H.PathTracer(W, Hh, max_bounce=8)
+    pt.upload(sc)
+    pt.render(1, spp, 0)
+    want = pt.read_rgba32f()
+    pt.close()
+    assert img.shape == want.shape
+    assert_bitwise(img, want, "%d-rank bench frame vs one context" % world)

@@ -77,9 +77,31 @@ def test_group_rejects_inconsistent_contexts(cornell_scene):
     a = H.PathTracer(32, 16, rank=0, world=2)
     b = H.PathTracer(40, 16, rank=1, world=2)
     c = H.PathTracer(32, 16, rank=0, world=2)
-    for trs in ([a, b], [a, c], [a]):
+    # render-affecting settings must agree too: the gathered frame is one render
+    d = H.PathTracer(32, 16, rank=1, world=2, max_bounce=3)
+    e_ = H.PathTracer(32, 16, rank=1, world=2, display_mode=2)
+    f = H.PathTracer(32, 16, rank=1, world=2, flags=H.PT_FLAG_NO_SKY)
+    g = H.PathTracer(32, 16, rank=1, world=2, rays_per_pixel=2)
+    for trs in ([a, b], [a, c], [a], [a, d], [a, e_], [a, f], [a, g]):
         with pytest.raises(H.PTError) as e:
             H.Group(trs)
         assert e.value.code == -1
-    for t in (a, b, c):
+    for t in (a, b, c, d, e_, f, g):
         t.close()
+
+
+def test_group_gather_time_excludes_renders(cornell_scene):
+    """pt_group_stats' gather time starts at the first pack copy, after the device streams
+    have waited for the contexts' renders (pt_group.h): a long render queued just before the
+    gather does not count."""
+    W, Hh, world = 640, 360, 2
+    g, trs = split_render(cornell_scene, W, Hh, world, 200)
+    g.gather()
+    ms, _ = g.stats()
+    for t in trs:
+        t.sync()
+    render_ms = max(t.timing()[0] for t in trs)
+    g.close()
+    for t in trs:
+        t.close()
+    assert render_ms > 5.0 and ms < 0.5 * render_ms, (ms, render_ms)

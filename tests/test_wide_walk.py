@@ -1,0 +1,93 @@
+"""CPU checks of the wide global-memory walk (pt_wide.h).
+
+tests/wide/wide_sim.cpp runs the kernel's own per-lane functions (ptw::wide_hits /
+wide_visit / wide_pop, compiled for the host) beside the reference's binary walk
+(calculateRayCollision, computeShader.c:367-432) on diffuse paths and adversarial rays, and
+fails on any segment whose closest t (bitwise) or triangle differs, or on any record child
+whose exact box test passes while the conservative test rejects it.  The GPU parity tests
+(tests/test_gpu_wide.py and every global-memory scene of the suite) then compare the kernel
+with the oracle.
+"""
+import json
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+import fuzz_scenes
+import pt_host as H
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+SRC = os.path.join(REPO, "tests", "wide", "wide_sim.cpp")
+WIDE_CPP = os.path.join(REPO, "opengl-path-tracing_amd", "csrc", "pt_wide.cpp")
+
+
+@pytest.fixture(scope="module")
+def sim(tmp_path_factory):
+    d = tmp_path_factory.mktemp("wide")
+    exe = str(d / "wide_sim")
+    subprocess.check_call(["g++", "-O2", "-std=c++17", "-ffp-contract=off", "-march=x86-64-v3", "-o", exe, SRC,
+                           WIDE_CPP])
+
+    def run(sb, stride=32, bounces=8, adversarial=5000):
+        path = str(d / "scene.bin")
+        with open(path, "wb") as f:
+            np.array([len(sb["tris"]), len(sb["nodes"]), len(sb["spheres"])], np.int32).tofile(f)
+            for k in ("tris", "nodes", "spheres", "cam"):
+                np.ascontiguousarray(sb[k], np.float32).tofile(f)
+        r = subprocess.run([exe, path, str(stride), str(bounces), str(adversarial)], capture_output=True, text=True)
+        assert r.returncode in (0, 1, 3), r.stderr
+        out = json.loads(r.stdout.strip().splitlines()[-1])
+        out["rc"], out["stderr"] = r.returncode, r.stderr
+        return out
+    return run
+
+
+def _ok(res):
+    assert res["rc"] == 0 and res["mismatches"] == 0 and res["cons_violations"] == 0, res["stderr"][:2000]
+
+
+def test_cornell(sim, cornell_scene):
+    res = sim(cornell_scene, stride=8, adversarial=20000)
+    _ok(res)
+    assert res["records"] >= 1 and res["segments"] > 20000
+
+
+def test_ship(sim, ship_scene):
+    _ok(sim(ship_scene, stride=16, adversarial=20000))
+
+
+@pytest.mark.parametrize("seed", range(40))
+def test_random_scenes(sim, seed):
+    """Triangle soups with flat quads, degenerate / duplicate triangles, floors and far-off
+    placements (tests/fuzz_scenes.py), sizes up to 9000 triangles."""
+    sc, _ = fuzz_scenes.random_case(seed)
+    if len(sc["nodes"]) == 0:
+        pytest.skip("no triangles")
+    _ok(sim(sc, stride=96, adversarial=3000))
+
+
+def test_stand_in_mesh(sim):
+    """A 6k-triangle bunny stand-in (the C3 generator at a smaller size): a deep tree whose
+    leaves the wide walk reaches through several record levels, partly outside LDS."""
+    import pt_scenes
+    obj, mtl = pt_scenes.write_scene("bunny", os.path.join(REPO, "scenes", "bunny_6000"), target_tris=6000)
+    res = sim(H.setupBuffers(obj, mtl), stride=48, adversarial=10000)
+    _ok(res)
+    # fewer record visits than the binary walk's node visits, and about as many leaves
+    assert res["wide_visits"] < 0.5 * res["ref_visits"]
+    assert res["wide_leaves"] < 1.2 * res["ref_leaves"] + 0.5
+
+
+def test_single_leaf_and_two_leaf_trees(sim):
+    """Roots that are a leaf (one record with one leaf child) and one internal node."""
+    for n in (1, 2, 3, 4):
+        tris = np.zeros((n, 16), np.float32)
+        for i in range(n):
+            tris[i, 0:3], tris[i, 4:7], tris[i, 8:11] = (i, 0, 0), (i + 1, 0, 1), (i, 1, 0.5)
+        mats = np.zeros((1, 16), np.float32)
+        mats[0, 0:3] = 0.5
+        sc = H.scene_from_arrays(tris, mats)
+        sc["cam"] = np.array([0.5, -6, 0.5, 0, 0.1, 1, 0.05, 0, 0, 0, 0, 0], np.float32)
+        _ok(sim(sc, stride=64, adversarial=4000))

@@ -27,6 +27,11 @@ for kv in a.key:
     k, v = (int(x) for x in kv.split("="))
     pt.set_key(k, v)
 pt.upload(sb)
+if os.environ.get("PMC_SEGMENTS"):   # the workload's segment count (counting build, same frames)
+    pt.set_counting(True)
+    pt.render(1, a.chunk, 0)
+    print("segments %d" % pt.stats()[1]["segments"], flush=True)
+    pt.set_counting(False)
 # the bench's step: frames 1..chunk from accumulate = 0, re-rendered (warm-up launch first)
 for i in range(a.launches + 1):
     pt.render(1, a.chunk, 0)

@@ -10,6 +10,7 @@ float4 per lane); WRITE_SIZE is exact for 16-B/lane stores.  Raw values are kept
 """
 import collections
 import csv
+import hashlib
 import json
 import os
 import sys
@@ -68,6 +69,13 @@ def main():
                 per["%s_ms_%s" % (kind, name)].append(v)
     avg = {k: sum(v) / len(v) for k, v in per.items()}
     out["counters_per_launch"] = avg
+    # the build these counters belong to: bench.py uses them only for this exact library
+    lib = os.path.join(REPO, "opengl-path-tracing_amd", "build", "libptrace.so")
+    with open(lib, "rb") as fh:
+        out["lib_sha256"] = hashlib.sha256(fh.read()).hexdigest()
+    ms = [v for k, v in avg.items() if k.startswith("launch_ms_")]
+    if ms:
+        out["pmc_launch_ms"] = sum(ms) / len(ms)
     if "FETCH_SIZE" in avg and "WRITE_SIZE" in avg:
         out["fetch_bytes_raw"] = avg["FETCH_SIZE"] * 1024
         out["write_bytes"] = avg["WRITE_SIZE"] * 1024
