@@ -14,6 +14,8 @@
  *                          (ncclGather of padded row blocks) and interleaved there by a
  *                          device kernel into the full RGBA32F frame, row 0 = bottom; the
  *                          result goes to host memory or stays in device memory
+ *   pt_group_gather_rgba8_aces / pt_group_present_*  the same frame through the reference's
+ *                          ACES view (screenQuadFrag.c:12-33), synchronous or pipelined
  * The gather waits for every context's stream (stream-ordered, no host round trip in
  * between) and returns once the frame is in `dst`.  The assembled frame is bit-identical to
  * a single context's render: each pixel's RNG depends only on (x, y, frame)
@@ -47,6 +49,21 @@ int pt_group_upload_scene(pt_group* g, const float* tris, int n_tris, const floa
 /* Full frame (height * width * 4 floats = `bytes` or more).  dst_on_device != 0: dst is device
  * memory on ctxs[0]'s device; else host memory. */
 int pt_group_gather_rgba32f(pt_group* g, float* dst, size_t bytes, int dst_on_device);
+
+/* The reference's view of the frame: the gathered frame through the ACES epilogue
+ * (screenQuadFrag.c:12-33) on the root device, RGBA8 with alpha 255 (height * width * 4
+ * bytes), in host or root-device memory -- the multi-GPU form of pt_read_rgba8_aces, so a
+ * display loop never tonemaps the 16-B-per-pixel frame on the host. */
+int pt_group_gather_rgba8_aces(pt_group* g, unsigned char* dst, size_t bytes, int dst_on_device);
+
+/* Pipelined presentation (the multi-GPU pt_present_begin / pt_present_end): begin enqueues the
+ * gather and the ACES epilogue of the frame as every context's stream has it now, then a copy
+ * into pinned host buffer `buf` (0..3) on a separate stream, and returns at once; renders
+ * queued afterwards wait only for the row packing.  end waits for that copy and returns the
+ * pinned pixels (valid until the buffer is begun again).  The gather time (pt_group_stats)
+ * is that of the last gather begun. */
+int pt_group_present_begin(pt_group* g, int buf);
+int pt_group_present_end(pt_group* g, int buf, const unsigned char** pixels);
 
 /* Device time of the last gather (ms, from the first pack copy to the interleaved frame on the
  * root device, HIP events) and the bytes each device sent. */

@@ -30,6 +30,9 @@ constexpr int kSceneBufs = 10;
 extern "C" int pt__scene_replicate_layout(pt_ctx* dst, const pt_ctx* src, void* dptr[kSceneBufs],
                                           const void* sptr[kSceneBufs], size_t bytes[kSceneBufs]);
 extern "C" int pt__scene_set_ready(pt_ctx* c, int ready);
+extern "C" int pt__aces_launch(const void* src, void* dst, long long n, void* stream);
+
+constexpr int kGroupPresentBufs = 4;   // pt_group_present_begin buffers
 
 namespace {
 
@@ -60,7 +63,16 @@ struct pt_group {
     float4* frame = nullptr;                // root: the frame for host destinations
     int* d_table = nullptr;                 // root: image rank -> block index
     std::vector<hipEvent_t> ctx_ev;         // per context, on its device
+    std::vector<hipEvent_t> packed_ev;      // per device: its contexts' rows are packed
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    // pipelined ACES presentation (pt_group_present_*): per buffer an RGBA8 frame on the root
+    // device, its pinned host copy and events, and one copy stream
+    uchar4* present_dev[kGroupPresentBufs] = {};
+    unsigned char* present_host[kGroupPresentBufs] = {};
+    hipEvent_t ev_tonemap[kGroupPresentBufs] = {}, ev_copied[kGroupPresentBufs] = {};
+    bool present_pending[kGroupPresentBufs] = {};
+    hipStream_t cstream = nullptr;
+    uchar4* rgba8 = nullptr;                // root: the ACES frame of pt_group_gather_rgba8_aces
     double last_ms = 0.0;
     std::string err;
 };
@@ -98,8 +110,22 @@ void pt_group_destroy(pt_group* g) {
         (void)hipSetDevice(g->devs[g->dev_idx[i]]);
         (void)hipEventDestroy(g->ctx_ev[i]);
     }
+    for (size_t d = 0; d < g->packed_ev.size(); d++) {
+        if (!g->packed_ev[d]) continue;
+        (void)hipSetDevice(g->devs[d]);
+        (void)hipEventDestroy(g->packed_ev[d]);
+    }
     if (!g->devs.empty()) {
         (void)hipSetDevice(g->devs[0]);
+        if (g->cstream) (void)hipStreamSynchronize(g->cstream);
+        for (int b = 0; b < kGroupPresentBufs; b++) {
+            (void)hipFree(g->present_dev[b]);
+            if (g->present_host[b]) (void)hipHostFree(g->present_host[b]);
+            if (g->ev_tonemap[b]) (void)hipEventDestroy(g->ev_tonemap[b]);
+            if (g->ev_copied[b]) (void)hipEventDestroy(g->ev_copied[b]);
+        }
+        if (g->cstream) (void)hipStreamDestroy(g->cstream);
+        (void)hipFree(g->rgba8);
         (void)hipFree(g->recv);
         (void)hipFree(g->frame);
         (void)hipFree(g->d_table);
@@ -161,10 +187,12 @@ int pt_group_create(pt_ctx* const* ctxs, int n, pt_group** out) {
     GNCCL(g, ncclCommInitAll(g->comm.data(), nd, g->devs.data()));
     g->stream.assign(nd, nullptr);
     g->send.assign(nd, nullptr);
+    g->packed_ev.assign(nd, nullptr);
     const size_t blk = block_floats(g) * sizeof(float);
     for (int d = 0; d < nd; d++) {
         GHIP(g, hipSetDevice(g->devs[d]));
         GHIP(g, hipStreamCreateWithFlags(&g->stream[d], hipStreamNonBlocking));
+        GHIP(g, hipEventCreateWithFlags(&g->packed_ev[d], hipEventDisableTiming));
         GHIP(g, hipMalloc(&g->send[d], std::max<size_t>(blk * (size_t)g->max_slots, 16)));
     }
     g->ctx_ev.assign(n, nullptr);
@@ -233,10 +261,14 @@ int pt_group_upload_scene(pt_group* g, const float* tris, int n_tris, const floa
     return PT_OK;
 }
 
-int pt_group_gather_rgba32f(pt_group* g, float* dst, size_t bytes, int dst_on_device) {
-    if (!g || !dst || g->ctx.empty()) return PT_E_ARG;
-    const size_t frame_bytes = (size_t)g->W * (size_t)g->H * sizeof(float4);
-    if (bytes < frame_bytes) return gfail(g, PT_E_ARG, "destination too small");
+}  // extern "C"
+
+// The gather, stream-ordered on the root device's stream: every device stream waits for its
+// contexts' pending renders, packs their rows, ncclGather collects the blocks on the root and
+// k_interleave_rows writes the frame to `out` (root device memory).  Each context's stream
+// then waits for its device's pack, so renders queued after this call cannot overwrite rows
+// that are still being packed.  Nothing is synchronised here.
+static int gather_core(pt_group* g, float4* out) {
     const int n = (int)g->ctx.size(), nd = (int)g->devs.size();
     const size_t blk = block_floats(g);
     // the device streams wait for every context's pending renders first; the timer starts
@@ -266,6 +298,16 @@ int pt_group_gather_rgba32f(pt_group* g, float* dst, size_t bytes, int dst_on_de
         if (ab) GHIP(g, hipMemcpyAsync(g->send[d] + (size_t)g->slot[i] * blk / 4, acc, ab, hipMemcpyDeviceToDevice,
                                        g->stream[d]));
     }
+    for (int d = 0; d < nd; d++) {
+        GHIP(g, hipSetDevice(g->devs[d]));
+        GHIP(g, hipEventRecord(g->packed_ev[d], g->stream[d]));
+    }
+    for (int i = 0; i < n; i++) {
+        void* cs = nullptr;
+        pt_stream(g->ctx[i], &cs);
+        GHIP(g, hipSetDevice(g->devs[g->dev_idx[i]]));
+        GHIP(g, hipStreamWaitEvent((hipStream_t)cs, g->packed_ev[g->dev_idx[i]], 0));
+    }
     GNCCL(g, ncclGroupStart());
     for (int d = 0; d < nd; d++) {
         if (hipSetDevice(g->devs[d]) != hipSuccess) { (void)ncclGroupEnd(); return gfail(g, PT_E_HIP, "hipSetDevice"); }
@@ -275,21 +317,93 @@ int pt_group_gather_rgba32f(pt_group* g, float* dst, size_t bytes, int dst_on_de
     }
     GNCCL(g, ncclGroupEnd());
     GHIP(g, hipSetDevice(g->devs[0]));
-    float4* out = dst_on_device ? (float4*)dst : g->frame;
     if (g->H > 0 && g->W > 0) {
         hipLaunchKernelGGL(k_interleave_rows, dim3((unsigned)((g->W + 255) / 256), (unsigned)g->H), dim3(256), 0,
                            g->stream[0], g->recv, g->d_table, out, g->W, g->world, g->rows_max);
         GHIP(g, hipGetLastError());
     }
     GHIP(g, hipEventRecord(g->ev1, g->stream[0]));
-    if (!dst_on_device) GHIP(g, hipMemcpyAsync(dst, g->frame, frame_bytes, hipMemcpyDeviceToHost, g->stream[0]));
-    for (int d = nd - 1; d >= 0; d--) {
+    return PT_OK;
+}
+
+// Drains the device streams (last one the root) and records the gather time.
+static int gather_finish(pt_group* g) {
+    for (int d = (int)g->devs.size() - 1; d >= 0; d--) {
         GHIP(g, hipSetDevice(g->devs[d]));
         GHIP(g, hipStreamSynchronize(g->stream[d]));
     }
     float ms = 0.0f;
     GHIP(g, hipEventElapsedTime(&ms, g->ev0, g->ev1));
     g->last_ms = ms;
+    return PT_OK;
+}
+
+extern "C" {
+
+int pt_group_gather_rgba32f(pt_group* g, float* dst, size_t bytes, int dst_on_device) {
+    if (!g || !dst || g->ctx.empty()) return PT_E_ARG;
+    const size_t frame_bytes = (size_t)g->W * (size_t)g->H * sizeof(float4);
+    if (bytes < frame_bytes) return gfail(g, PT_E_ARG, "destination too small");
+    float4* out = dst_on_device ? (float4*)dst : g->frame;
+    int rc = gather_core(g, out);
+    if (rc) return rc;
+    if (!dst_on_device) GHIP(g, hipMemcpyAsync(dst, g->frame, frame_bytes, hipMemcpyDeviceToHost, g->stream[0]));
+    return gather_finish(g);
+}
+
+int pt_group_gather_rgba8_aces(pt_group* g, unsigned char* dst, size_t bytes, int dst_on_device) {
+    if (!g || !dst || g->ctx.empty()) return PT_E_ARG;
+    const long long n = (long long)g->W * (long long)g->H;
+    if (bytes < (size_t)n * 4) return gfail(g, PT_E_ARG, "destination too small");
+    GHIP(g, hipSetDevice(g->devs[0]));
+    if (!g->rgba8 && !dst_on_device) GHIP(g, hipMalloc(&g->rgba8, std::max<long long>(n, 1) * sizeof(uchar4)));
+    int rc = gather_core(g, g->frame);
+    if (rc) return rc;
+    void* out = dst_on_device ? (void*)dst : (void*)g->rgba8;
+    rc = pt__aces_launch(g->frame, out, n, g->stream[0]);
+    if (rc) return gfail(g, rc, "k_aces launch");
+    if (!dst_on_device && n) GHIP(g, hipMemcpyAsync(dst, g->rgba8, (size_t)n * 4, hipMemcpyDeviceToHost, g->stream[0]));
+    return gather_finish(g);
+}
+
+int pt_group_present_begin(pt_group* g, int buf) {
+    if (!g || g->ctx.empty()) return PT_E_ARG;
+    if (buf < 0 || buf >= kGroupPresentBufs) return gfail(g, PT_E_ARG, "present buffer must be 0..3");
+    const long long n = (long long)g->W * (long long)g->H;
+    GHIP(g, hipSetDevice(g->devs[0]));
+    if (!g->cstream) GHIP(g, hipStreamCreateWithFlags(&g->cstream, hipStreamNonBlocking));
+    if (!g->present_dev[buf]) {
+        GHIP(g, hipMalloc(&g->present_dev[buf], std::max<long long>(n, 1) * sizeof(uchar4)));
+        GHIP(g, hipHostMalloc((void**)&g->present_host[buf], std::max<long long>(n, 1) * sizeof(uchar4),
+                              hipHostMallocDefault));
+        GHIP(g, hipEventCreateWithFlags(&g->ev_tonemap[buf], hipEventDisableTiming));
+        GHIP(g, hipEventCreateWithFlags(&g->ev_copied[buf], hipEventDisableTiming));
+    }
+    // a buffer begun again before its end: its previous copy must land first
+    if (g->present_pending[buf]) GHIP(g, hipEventSynchronize(g->ev_copied[buf]));
+    g->present_pending[buf] = false;
+    int rc = gather_core(g, g->frame);
+    if (rc) return rc;
+    GHIP(g, hipSetDevice(g->devs[0]));
+    rc = pt__aces_launch(g->frame, g->present_dev[buf], n, g->stream[0]);
+    if (rc) return gfail(g, rc, "k_aces launch");
+    GHIP(g, hipEventRecord(g->ev_tonemap[buf], g->stream[0]));
+    GHIP(g, hipStreamWaitEvent(g->cstream, g->ev_tonemap[buf], 0));
+    if (n) GHIP(g, hipMemcpyAsync(g->present_host[buf], g->present_dev[buf], (size_t)n * 4, hipMemcpyDeviceToHost,
+                                  g->cstream));
+    GHIP(g, hipEventRecord(g->ev_copied[buf], g->cstream));
+    g->present_pending[buf] = true;
+    return PT_OK;
+}
+
+int pt_group_present_end(pt_group* g, int buf, const unsigned char** pixels) {
+    if (!g || !pixels) return PT_E_ARG;
+    if (buf < 0 || buf >= kGroupPresentBufs) return gfail(g, PT_E_ARG, "present buffer must be 0..3");
+    if (!g->present_pending[buf]) return gfail(g, PT_E_STATE, "pt_group_present_end without pt_group_present_begin");
+    GHIP(g, hipSetDevice(g->devs[0]));
+    GHIP(g, hipEventSynchronize(g->ev_copied[buf]));
+    g->present_pending[buf] = false;
+    *pixels = g->present_host[buf];
     return PT_OK;
 }
 

@@ -278,15 +278,6 @@ extern __shared__ float4 g_lds[];   // the state-machine kernel's scene copy (no
 #ifndef PT_PAD_NODES
 #define PT_PAD_NODES 67
 #endif
-#ifndef PT_FLAGS_IN_STATE
-#define PT_FLAGS_IN_STATE 1
-#endif
-#ifndef PT_FAST_FROM_RD
-#define PT_FAST_FROM_RD 1
-#endif
-#ifndef PT_GWALK_FLAT
-#define PT_GWALK_FLAT 1
-#endif
 constexpr int kPadNodes = PT_PAD_NODES;
 typedef float v4f __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) const v4f lds_v4f;
@@ -329,14 +320,11 @@ __device__ __forceinline__ bool in_range_abs(float v, float lo, float hi) {
     return (a >= lo) & (a <= hi);
 }
 
-// The box tests' "tn <= tf && tn <= t" is evaluated as tn <= min(tf, t) (PT_CONS_MED3, default):
+// The box tests' "tn <= tf && tn <= t" is evaluated as tn <= min(tf, t):
 // one compare instead of two plus a scalar AND of their lane masks, which sat on the walk
 // step's dependency chain (vector compare -> scalar AND -> vector select -> next LDS read):
 // +1.5..2% on C2.  v_med3(tf, t, -inf) is min(tf, t) for non-NaN operands; inside the
 // exact-reciprocal guard every quotient is finite, and t is finite or +inf.
-#ifndef PT_CONS_MED3
-#define PT_CONS_MED3 1
-#endif
 // Scalar on purpose: packed f32 (v_pk_fma_f32) takes two passes on gfx950's SIMD-32, so
 // it saves issue slots but no VALU cycles, and its broadcast operand pairs cost registers
 // (measured: no gain, spills).  t is compared, not folded into the min3: fminf on a
@@ -347,11 +335,7 @@ __device__ __forceinline__ bool slab_fast(float4 A, float4 B, f3 o, f3 d, f3 rd,
     float z0 = qdiv(B.x - o.z, d.z, rd.z), z1 = qdiv(B.y - o.z, d.z, rd.z);
     float tn = fmaxf(fmaxf(fminf(x0, x1), fminf(y0, y1)), fminf(z0, z1));
     float tf = fminf(fminf(fmaxf(x0, x1), fmaxf(y0, y1)), fmaxf(z0, z1));
-#if PT_CONS_MED3
     return tn <= __builtin_amdgcn_fmed3f(tf, cur_t, -__builtin_huge_valf());   // as slab_oct_cons
-#else
-    return tn <= tf && tn <= cur_t;
-#endif
 }
 
 // Slab test on an octant image of the LDS walk (WalkLinks): the node's bounds are stored
@@ -366,71 +350,31 @@ __device__ __forceinline__ bool slab_oct(float4 A, float4 B, f3 o, f3 d, f3 rd, 
     float zn = qdiv(B.x - o.z, d.z, rd.z), zf = qdiv(B.y - o.z, d.z, rd.z);
     float tn = fmaxf(fmaxf(xn, yn), zn);
     float tf = fminf(fminf(xf, yf), zf);
-#if PT_CONS_MED3
     return tn <= __builtin_amdgcn_fmed3f(tf, cur_t, -__builtin_huge_valf());   // as slab_oct_cons
-#else
-    return tn <= tf && tn <= cur_t;
-#endif
 }
 
 // Conservative slab_oct of the culling walk.  Inside the exact-reciprocal
 // guard every quotient is finite and normal or zero.  With u = 2^-24, q = RN(RN(b - o) / d)
-// the exact quotient and rd = RN(1/d):
-//   PT_CONS_FMA = 0: q0 = RN(RN(b - o) * rd) lies within 4u |q| of q (three relative
-//                    roundings); lo = tn0 - 2^-20 |tn0| <= tn and hi = tf0 + 2^-20 |tf0| >= tf,
-//                    where tn0 / tf0 are the max / min of the near / far q0 (max and min only
-//                    select, so tn0 <= tn + 4.1u |tn| and tf0 >= tf - 4.1u |tf|);
-//   PT_CONS_FMA = 1: q0 = fma(b, rd, ord) with ord = RN(-o * rd) lies within
-//                    4.1u |q| + 1.1u |ord|; lo and hi as above, less / plus E = 2^-22 max|ord|;
-//   PT_CONS_FMA = 2 (default): the margin is folded into per-axis addends, no per-node
-//                    margin: near = fma(b, rd, ord - E_i), far = fma(b, rd, ord + E_i) with
-//                    E_i = 2^-19 M_i |rd_i| + 2^-17 |ord_i| (M_i: the largest |coordinate| of
-//                    the scene on axis i, so |b - o| <= M_i + |o_i| and
-//                    |q| <= M_i |rd_i| + 1.01 |ord_i|): the error of every fma quotient,
-//                    4.2u |q| + 2.1u |ord| + 2.1u E_i including the rounding of ord -+ E_i,
-//                    is below E_i, so near <= q_near and far >= q_far on every axis.
-// Either way an exact hit (tn <= tf and tn <= t) is always a hit here.  Only culling may use
-// it: a node it accepts and the exact test rejects is walked in vain, and a leaf reached
-// that way is rejected by the exact test of its own box, which the leaf phase runs before a
-// triangle moves t.
-#ifndef PT_CONS_FMA
-#define PT_CONS_FMA 2
-#endif
-#ifndef PT_YIELD_LEAN
-#define PT_YIELD_LEAN 1
-#endif
-#if PT_CONS_FMA != 2
-constexpr float kConsEta = 0x1p-20f;
-#endif
-// ol / oh: the per-ray addends (form 1: ord, ord; form 2: ord - E_i, ord + E_i); E: form 1's margin
-__device__ __forceinline__ bool slab_oct_cons(float4 A, float4 B, f3 o, f3 rd, f3 ol, f3 oh, float E, float cur_t) {
-#if PT_CONS_FMA
-    (void)o;
+// the exact quotient and rd = RN(1/d), the margin is folded into per-axis addends:
+// near = fma(b, rd, ord - E_i), far = fma(b, rd, ord + E_i) with ord = RN(-o * rd) and
+// E_i = 2^-19 M_i |rd_i| + 2^-17 |ord_i| (M_i: the largest |coordinate| of the scene on axis i,
+// so |b - o| <= M_i + |o_i| and |q| <= M_i |rd_i| + 1.01 |ord_i|): the error of every fma
+// quotient, 4.2u |q| + 2.1u |ord| + 2.1u E_i including the rounding of ord -+ E_i, is below
+// E_i, so near <= q_near and far >= q_far on every axis, and an exact hit (tn <= tf and
+// tn <= t) is always a hit here.  Only culling may use it: a node it accepts and the exact
+// test rejects is walked in vain, and a leaf reached that way is rejected by the exact test
+// of its own box, which the leaf phase runs before a triangle moves t.  (Measured forms:
+// RN(b - o) * rd with a relative margin per node +2.2%, fma with a per-node margin +4.7%,
+// this one +7.1% on C2 over the exact test.)
+// ol / oh: the per-ray addends ord - E_i, ord + E_i
+__device__ __forceinline__ bool slab_oct_cons(float4 A, float4 B, f3 rd, f3 ol, f3 oh, float cur_t) {
     float xn = __builtin_fmaf(A.x, rd.x, ol.x), xf = __builtin_fmaf(A.y, rd.x, oh.x);
     float yn = __builtin_fmaf(A.z, rd.y, ol.y), yf = __builtin_fmaf(A.w, rd.y, oh.y);
     float zn = __builtin_fmaf(B.x, rd.z, ol.z), zf = __builtin_fmaf(B.y, rd.z, oh.z);
-#else
-    (void)ol;
-    (void)oh;
-    float xn = (A.x - o.x) * rd.x, xf = (A.y - o.x) * rd.x;
-    float yn = (A.z - o.y) * rd.y, yf = (A.w - o.y) * rd.y;
-    float zn = (B.x - o.z) * rd.z, zf = (B.y - o.z) * rd.z;
-#endif
     float tn = fmaxf(fmaxf(xn, yn), zn);
     float tf = fminf(fminf(xf, yf), zf);
-#if PT_CONS_FMA == 2
-    (void)E;
-#if PT_CONS_MED3
-    // one compare (PT_CONS_MED3); fminf would add a canonicalizing v_max on the loop-carried t
+    // one compare; fminf would add a canonicalizing v_max on the loop-carried t
     return tn <= __builtin_amdgcn_fmed3f(tf, cur_t, -__builtin_huge_valf());
-#else
-    return tn <= tf && tn <= cur_t;
-#endif
-#else
-    float lo = __builtin_fmaf(-kConsEta, __builtin_fabsf(tn), tn) - E;
-    float hi = __builtin_fmaf(kConsEta, __builtin_fabsf(tf), tf) + E;
-    return lo <= hi && lo <= cur_t;
-#endif
 }
 
 // Byte offset of the ray's octant image in the LDS walk: image k = sx | sy << 1 | sz << 2
@@ -573,9 +517,6 @@ constexpr int kQueueStride = 32;
 #ifndef PT_WALK_UNROLL
 #define PT_WALK_UNROLL 4
 #endif
-#ifndef PT_WALK_SINKS
-#define PT_WALK_SINKS 1     // the culling walk steps unmasked over its sink images
-#endif
 #ifndef PT_SINK_UNROLL
 #define PT_SINK_UNROLL 6    // its node steps per yield check (measured: 4 -2.2%, 8 -1.4% against 6)
 #endif
@@ -602,11 +543,7 @@ __device__ __forceinline__ void trav_walk(const SceneView& S, f3 o, f3 d, f3 rd,
                                           bool eligible = true) {
     const int min_thresh = leaf_thresh < shade_thresh ? leaf_thresh : shade_thresh;
     f3 ol = mk(0, 0, 0), oh = mk(0, 0, 0);
-    float E = 0.0f;
-    if (CONS && PT_CONS_FMA == 1) {
-        ol = oh = mk(-(o.x * rd.x), -(o.y * rd.y), -(o.z * rd.z));
-        E = 0x1p-22f * fmaxf(fmaxf(__builtin_fabsf(ol.x), __builtin_fabsf(ol.y)), __builtin_fabsf(ol.z));
-    } else if (CONS && PT_CONS_FMA == 2) {   // S.cm[i] = 2^-19 M_i (slab_oct_cons)
+    if (CONS) {   // S.cm[i] = 2^-19 M_i (slab_oct_cons)
         const f3 ord = mk(-(o.x * rd.x), -(o.y * rd.y), -(o.z * rd.z));
         const f3 e = mk(__builtin_fmaf(S.cm[0], __builtin_fabsf(rd.x), 0x1p-17f * __builtin_fabsf(ord.x)),
                         __builtin_fmaf(S.cm[1], __builtin_fabsf(rd.y), 0x1p-17f * __builtin_fabsf(ord.y)),
@@ -631,21 +568,18 @@ __device__ __forceinline__ void trav_walk(const SceneView& S, f3 o, f3 d, f3 rd,
     const unsigned long long pre_leaf = LDS ? m_leaf : __ballot(st == ST_LEAF);
     const unsigned long long pre_shade = LDS ? m_shade : __ballot(st == ST_SHADE);
     int w = walking ? bi : (CONS ? sink0 : -1);
-#if PT_YIELD_LEAN
     // the yield test in counts: the walkers (ballot of w < sink0, or w >= 0) are live lanes, so
     // the lanes waiting elsewhere number popc(live) - walkers, and "waiting >= min_thresh" is
     // walkers <= popc(live) - min_thresh; floor1 >= 1 also covers "no walker left" (fewer
     // scalar instructions per yield check than the mask form)
     const int floor1 = trav_floor > 1 ? trav_floor : 1;
     const int wait_lim = __popcll(live) - min_thresh;
-#endif
-#if PT_WALK_SINKS
     if (CONS) {
         auto sstep = [&]() {
             float4 lo, hi;
             node_at<LDS, PADN>(S, w, lo, hi);
             const int a = __float_as_int(hi.z), b = __float_as_int(hi.w);
-            const bool hb = (ALL_FAST || fast) ? slab_oct_cons(lo, hi, o, rd, ol, oh, E, t) : slab(lo, hi, o, d, t);
+            const bool hb = (ALL_FAST || fast) ? slab_oct_cons(lo, hi, rd, ol, oh, t) : slab(lo, hi, o, d, t);
 #ifdef PT_PHASE_CLOCK
             if (w < sink0) diag_tick(c.tw, c.tl);
 #endif
@@ -654,16 +588,9 @@ __device__ __forceinline__ void trav_walk(const SceneView& S, f3 o, f3 d, f3 rd,
         for (;;) {
 #pragma unroll
             for (int u = 0; u < PT_SINK_UNROLL; u++) sstep();
-#if PT_YIELD_LEAN
             const int nw = __popcll(__ballot(w < sink0));
             if (nw < floor1) break;
             if (nw <= wait_lim) {
-#else
-            unsigned long long mt = __ballot(w < sink0);
-            if (!mt) break;
-            if (__popcll(mt) < trav_floor) break;
-            if (__popcll(live & ~mt) >= min_thresh) {
-#endif
                 if (__popcll(pre_leaf | __ballot(w > sink0)) >= leaf_thresh) break;
                 if (__popcll(pre_shade | (__ballot(w == sink0) & mw)) >= shade_thresh) break;
             }
@@ -675,9 +602,7 @@ __device__ __forceinline__ void trav_walk(const SceneView& S, f3 o, f3 d, f3 rd,
         }
         return;
     }
-#endif
     auto step = [&]() {
-#if PT_GWALK_FLAT
         if (!LDS && !COUNT && ALL_FAST) {
             // global-memory walk without the per-step exec-mask branch: a lane whose walk has
             // stopped (w < 0) steps on the root, an LDS top node (S.np >= 1 for any tree), and
@@ -691,12 +616,11 @@ __device__ __forceinline__ void trav_walk(const SceneView& S, f3 o, f3 d, f3 rd,
             w = on ? (hb ? (a >= 0 ? a : -3 - b) : b) : w;
             return;
         }
-#endif
         if (w >= 0) {
             float4 lo, hi;
             node_at<LDS, PADN>(S, w, lo, hi);
             int a = __float_as_int(hi.z), b = __float_as_int(hi.w);
-            bool hb = (ALL_FAST || fast) ? (LDS ? (CONS ? slab_oct_cons(lo, hi, o, rd, ol, oh, E, t)
+            bool hb = (ALL_FAST || fast) ? (LDS ? (CONS ? slab_oct_cons(lo, hi, rd, ol, oh, t)
                                                         : slab_oct(lo, hi, o, d, rd, t))
                                                  : slab_fast(lo, hi, o, d, rd, t))
                                          : slab(lo, hi, o, d, t);
@@ -715,16 +639,9 @@ __device__ __forceinline__ void trav_walk(const SceneView& S, f3 o, f3 d, f3 rd,
     for (;;) {
 #pragma unroll
         for (int u = 0; u < kWalkUnroll; u++) step();
-#if PT_YIELD_LEAN
         const int nw = __popcll(__ballot(w >= 0));
         if (nw < floor1) break;                   // too few walkers (or none): run a waiting phase
         if (nw <= wait_lim) {
-#else
-        unsigned long long mt = __ballot(w >= 0);
-        if (!mt) break;
-        if (__popcll(mt) < trav_floor) break;     // too few walkers: run a waiting phase
-        if (__popcll(live & ~mt) >= min_thresh) {
-#endif
             if (__popcll(pre_leaf | __ballot(w <= -2)) >= leaf_thresh) break;
             if (__popcll(pre_shade | (__ballot(w == -1) & mw)) >= shade_thresh) break;
         }
@@ -751,6 +668,11 @@ __device__ __forceinline__ void trav_walk(const SceneView& S, f3 o, f3 d, f3 rd,
 #define PT_WIDE_STACK 2
 #endif
 constexpr int kWideStack = PT_WIDE_STACK;
+// float4 per device record: the three quads of pt_wide.h packed (48 B) or on a 64-B stride
+#ifndef PT_WIDE_STRIDE
+#define PT_WIDE_STRIDE 4
+#endif
+constexpr int kWideStride = PT_WIDE_STRIDE;
 #ifndef PT_WIDE_UNROLL
 #define PT_WIDE_UNROLL 2
 #endif
@@ -764,7 +686,7 @@ __device__ __forceinline__ void wrec_at(const SceneView& S, int n, float4& q0, f
         q1 = make_float4(y.x, y.y, y.z, y.w);
         q2 = make_float4(z.x, z.y, z.z, z.w);
     } else {
-        const float4* r = S.wrec + 4 * n;
+        const float4* r = S.wrec + kWideStride * n;
         q0 = r[0];
         q1 = r[1];
         q2 = r[2];
@@ -840,7 +762,7 @@ __global__ __launch_bounds__(NT, MINW) void k_render_sm(KParams p) {
         if ((unsigned)(size_t)(__attribute__((address_space(3))) const char*)g_lds != 0u) __builtin_trap();
         // 8 octant images (the culling walk: + its sink image)
         const int N = PADN ? kPadNodes : p.walk_np, T = p.n_slots, nt = 4 * T;
-        const bool sk = PT_WALK_SINKS && !COUNT && p.cons_walk;
+        const bool sk = !COUNT && p.cons_walk;
         const int nn = sk ? 18 * N : 16 * N;
         const float4* wsrc = sk ? p.sc.walk_sk : p.sc.walk_lds;
         const int nm = 3 * p.n_mats, ns = 2 * p.sc.n_spheres;
@@ -874,7 +796,7 @@ __global__ __launch_bounds__(NT, MINW) void k_render_sm(KParams p) {
         // lanes outside the guard reads every node from global memory
         const int K = WIDE ? p.wide_top : p.n_top;
         if (WIDE) {
-            for (int i = threadIdx.x; i < 3 * K; i += blockDim.x) lds[(i % 3) * K + i / 3] = p.sc.wrec[4 * (i / 3) + i % 3];
+            for (int i = threadIdx.x; i < 3 * K; i += blockDim.x) lds[(i % 3) * K + i / 3] = p.sc.wrec[kWideStride * (i / 3) + i % 3];
         } else {
             for (int i = threadIdx.x; i < 2 * K; i += blockDim.x) lds[(i & 1) * K + (i >> 1)] = p.sc.nodes[i];
         }
@@ -913,21 +835,12 @@ __global__ __launch_bounds__(NT, MINW) void k_render_sm(KParams p) {
 
     Cnt c = {0, 0, 0, 0, 0};
     int st = ST_SHADE;
-#if PT_FLAGS_IN_STATE
     // "fresh" (SHADE without a segment to finish: start / after shading) is t < 0, and "a new
     // camera ray is due" is bounce < 0: no lane-mask booleans carried around the loop (their
     // merges cost scalar instructions on every iteration)
-#define PT_FRESH (t < 0.0f)
-#define PT_NEED_RAY (bounce < 0)
-#else
-    bool fresh = true;        // SHADE without a finished segment (start / after fetch)
-    bool need_ray = true;     // next SHADE must start a new camera ray
-#define PT_FRESH fresh
-#define PT_NEED_RAY need_ray
-#endif
     int lx = -1, y = 0;
     int aidx = 0;             // rows_local * W < 2^31 (checked at pt_create)
-    int k = 0, kend = 0, r = 0, bounce = PT_FLAGS_IN_STATE ? -1 : 0;   // frames k..kend-1 of this work item
+    int k = 0, kend = 0, r = 0, bounce = -1;   // frames k..kend-1 of this work item
     unsigned qnext = 0, qend = 0;             // wave's reserved queue ids (frame-split mode)
     unsigned tile_id = 0, pcost = 0;    // adaptive queue order: this pixel's tile + segments
     float4 acc = make_float4(0, 0, 0, 0);
@@ -938,11 +851,8 @@ __global__ __launch_bounds__(NT, MINW) void k_render_sm(KParams p) {
     // the reference performs when it accepts the hit (o + d*t; the stored/recomputed
     // normal and its flip against d; matIdx), on the same final t -- the same bits.
     //   hprim >= 0: triangle slot, -1: no hit, <= -2: sphere (-2 - index)
-#if !PT_FAST_FROM_RD
-    bool fast = false;
-#endif
     f3 rd = mk(0, 0, 0);
-    float t = PT_FLAGS_IN_STATE ? -1.0f : 0.0f;
+    float t = -1.0f;
     int hprim = -1, bi = -1, leaf = 0;   // bi: walk position (WalkLinks); leaf: code of a hit leaf
     // wide walk (lanes inside the guard): bi is its position (pt_wide.h), plus the stack and R
     uint32_t we[kWideStack] = {};
@@ -952,11 +862,9 @@ __global__ __launch_bounds__(NT, MINW) void k_render_sm(KParams p) {
     unsigned long long clk[6] = {0, 0, 0, 0, 0, 0};   // cycles + wave iterations per phase
 #endif
     for (;;) {
-#if PT_FAST_FROM_RD
         // inside the exact-reciprocal guard (the segment's "fast" walk) <=> rd was set: |d_i| is
         // in [2^-20, 2] there, so RN(1/d_x) is nonzero; outside it rd stays 0
         const bool fast = rd.x != 0.0f;
-#endif
         const unsigned long long mS = __ballot(st == ST_SHADE), mL = __ballot(st == ST_LEAF), mT = __ballot(st == ST_TRAV);
         int nS = __popcll(mS);
         int nL = __popcll(mL);
@@ -974,7 +882,7 @@ __global__ __launch_bounds__(NT, MINW) void k_render_sm(KParams p) {
         const bool low = nT < p.trav_floor;
         if (nS > 0 && (nS >= p.shade_thresh || (low && nL == 0))) {
             // ---------------- SHADE: finish segment, regenerate, set up next segment
-            if (st == ST_SHADE && !PT_FRESH) {
+            if (st == ST_SHADE && !(t < 0.0f)) {   // a finished segment (t < 0: fresh)
                 const bool hit = hprim != -1;
                 if (COUNT) { c.seg++; if (hit) c.hits++; diag_tick(c.sw, c.sl); }
                 pcost++;
@@ -1036,11 +944,7 @@ __global__ __launch_bounds__(NT, MINW) void k_render_sm(KParams p) {
                     rgb = inc + env * col;
                     finished = true;
                 }
-#if PT_FLAGS_IN_STATE
                 if (finished) bounce = -1;
-#else
-                need_ray = finished;
-#endif
                 if (finished) {
                     bool frame_done = true;
                     f3 px;
@@ -1068,13 +972,9 @@ __global__ __launch_bounds__(NT, MINW) void k_render_sm(KParams p) {
                         k++;
                     }
                 }
-#if PT_FLAGS_IN_STATE
                 t = -1.0f;
-#else
-                fresh = true;
-#endif
             }
-            if ((st == ST_SHADE) & PT_NEED_RAY & (lx >= 0) & (k >= (SPLIT ? kend : p.n_frames))) {
+            if ((st == ST_SHADE) & (bounce < 0) & (lx >= 0) & (k >= (SPLIT ? kend : p.n_frames))) {
                 if (!SPLIT) p.accum[aidx] = acc;
                 if (p.tile_cost && tile_id != ~0u) atomicAdd(&p.tile_cost[tile_id], pcost);
                 lx = -1;
@@ -1145,17 +1045,13 @@ __global__ __launch_bounds__(NT, MINW) void k_render_sm(KParams p) {
                             r = 0;
                             psum = mk(0, 0, 0);
                             if (!SPLIT) acc = p.acc_first ? p.accum[aidx] : make_float4(0, 0, 0, 0);
-#if PT_FLAGS_IN_STATE
                             bounce = -1;
-#else
-                            need_ray = true;
-#endif
                         }
                     }
                 }
             }
             if (st == ST_SHADE && lx >= 0) {
-                if (PT_NEED_RAY) {    // camera ray (:514-542)
+                if (bounce < 0) {    // camera ray due (:514-542)
                     if (r == 0) state = pt::seed(lx, y, p.frame_first + k);
                     float ax = 0.0f, ay = 0.0f;
                     if (!(p.flags & PT_FLAG_NO_AA)) {
@@ -1172,33 +1068,19 @@ __global__ __launch_bounds__(NT, MINW) void k_render_sm(KParams p) {
                     inc = mk(0, 0, 0);
                     col = mk(1, 1, 1);
                     bounce = 0;
-#if !PT_FLAGS_IN_STATE
-                    need_ray = false;
-#endif
                 }
                 // segment set-up: exact-reciprocal guard, spheres (:372-385), walk start
                 // the ray half of the guard, evaluated without short-circuit branches (each
                 // && of the old form was an exec-mask branch): every origin component 0 or
                 // in [2^-40, 2^60], every direction component in [2^-20, 2] (NaN fails)
-#if PT_FAST_FROM_RD
                 const bool fast_seg =
-#else
-                fast =
-#endif
                        (p.scene_fast != 0) & in_guard(o.x, 0x1p-40f, 0x1p60f) & in_guard(o.y, 0x1p-40f, 0x1p60f) &
                        in_guard(o.z, 0x1p-40f, 0x1p60f) & in_range_abs(d.x, 0x1p-20f, 2.0f) &
                        in_range_abs(d.y, 0x1p-20f, 2.0f) & in_range_abs(d.z, 0x1p-20f, 2.0f);
-#if PT_FAST_FROM_RD
-#define PT_FAST_SEG fast_seg
                 // under the guard |d_i| is in [2^-20, 2]: rcp_fast is the exact RN(1/d_i); rd = 0
                 // marks a segment outside it
                 rd = fast_seg ? mk(pt::rcp_fast(d.x), pt::rcp_fast(d.y), pt::rcp_fast(d.z)) : mk(0, 0, 0);
-#else
-#define PT_FAST_SEG fast
-                // under the guard |d_i| is in [2^-20, 2]: rcp_fast is the exact RN(1/d_i)
-                if (fast) rd = mk(pt::rcp_fast(d.x), pt::rcp_fast(d.y), pt::rcp_fast(d.z));
-#endif
-                if (COUNT && !PT_FAST_SEG) c.slow++;
+                if (COUNT && !fast_seg) c.slow++;
                 if (COUNT && ray_has_nan(o, d)) c.nan++;
                 t = __builtin_huge_valf();
                 hprim = -1;
@@ -1218,17 +1100,14 @@ __global__ __launch_bounds__(NT, MINW) void k_render_sm(KParams p) {
                         }
                     }
                 }
-#if !PT_FLAGS_IN_STATE
-                fresh = false;
-#endif
                 const bool walk = use_tris & (COUNT || !ray_has_nan(o, d));
                 // inside the root box (all three axes, inclusive) each axis has near <= 0 <=
                 // far, so the exact slab says hit for any t >= 0: skip the root's test
-                const bool inside = (root_skip >= 0) & PT_FAST_SEG & (o.x >= p.root_box[0]) & (o.x <= p.root_box[1]) &
+                const bool inside = (root_skip >= 0) & fast_seg & (o.x >= p.root_box[0]) & (o.x <= p.root_box[1]) &
                                     (o.y >= p.root_box[2]) & (o.y <= p.root_box[3]) & (o.z >= p.root_box[4]) &
                                     (o.z <= p.root_box[5]);
-                const int img = (LDS && PT_FAST_SEG) ? oct_base(d, S.np << 5) : 0;   // octant image
-                bi = walk ? ((WIDE && PT_FAST_SEG) ? 0 : (inside ? root_skip : 0) + img) : -1;
+                const int img = (LDS && fast_seg) ? oct_base(d, S.np << 5) : 0;   // octant image
+                bi = walk ? ((WIDE && fast_seg) ? 0 : (inside ? root_skip : 0) + img) : -1;
                 if (WIDE) {   // the wide walk starts at the root record with an empty stack
 #pragma unroll
                     for (int k = 0; k < kWideStack; k++) we[k] = 0u;
@@ -1252,7 +1131,7 @@ __global__ __launch_bounds__(NT, MINW) void k_render_sm(KParams p) {
                     s0 = gc & ~1;                            // slots 2g, 2g+1
                     cop = (gc & 1) != 0;
                 }
-                if (PT_WALK_SINKS && LDS && !COUNT && p.cons_walk) {   // sinks carry the pair k only
+                if (LDS && !COUNT && p.cons_walk) {   // sinks carry the pair k only
                     s0 = 2 * leaf;
                     cop = __float_as_int(tri_quad<LDS>(S, s0 + 1, 1).w) != 0;
                 }
@@ -1497,6 +1376,7 @@ struct pt_ctx {
     int n_wide = 0;                 // wide index space (records + leaves)
     float wide_cw[3] = {0, 0, 0};
     int wide_off = 0;               // tuning key 16: 1 = the binary global walk
+    int wide_threads = 0;           // tuning key 17: threads per block of the wide walk (0 = automatic)
     unsigned long long* d_counters = nullptr;
     unsigned int* d_work = nullptr;
     int* d_frame = nullptr;                      // progressive graph frame counter
@@ -1947,11 +1827,17 @@ int pt_upload_scene(pt_ctx* c, const float* tris, int n_tris, const float* bvh, 
     free_scene(c);
     if (wide) {
         const size_t nr = (size_t)wt.n_index;
-        HIPCHK(c, hipMalloc(&c->d_wrec, nr * 4 * sizeof(float4)));
+        HIPCHK(c, hipMalloc(&c->d_wrec, nr * kWideStride * sizeof(float4)));
         HIPCHK(c, hipMalloc(&c->d_wlbox, nr * 2 * sizeof(float4)));
         HIPCHK(c, hipMalloc(&c->d_nodesw, dnw.size() * sizeof(float4)));
         HIPCHK(c, hipMalloc(&c->d_trisw, dtw.size() * sizeof(float4)));
-        HIPCHK(c, hipMemcpy(c->d_wrec, wt.rec.data(), nr * 4 * sizeof(float4), hipMemcpyHostToDevice));
+        if (kWideStride != 4) {   // pack the three used quads of each 64-B host record
+            std::vector<float> packed(nr * kWideStride * 4);
+            for (size_t i = 0; i < nr; i++)
+                std::memcpy(&packed[i * kWideStride * 4], &wt.rec[i * 16], kWideStride * 16);
+            wt.rec.swap(packed);
+        }
+        HIPCHK(c, hipMemcpy(c->d_wrec, wt.rec.data(), nr * kWideStride * sizeof(float4), hipMemcpyHostToDevice));
         HIPCHK(c, hipMemcpy(c->d_wlbox, wt.lbox.data(), nr * 2 * sizeof(float4), hipMemcpyHostToDevice));
         HIPCHK(c, hipMemcpy(c->d_nodesw, dnw.data(), dnw.size() * sizeof(float4), hipMemcpyHostToDevice));
         HIPCHK(c, hipMemcpy(c->d_trisw, dtw.data(), dtw.size() * sizeof(float4), hipMemcpyHostToDevice));
@@ -2084,6 +1970,13 @@ int pt_set_tuning(pt_ctx* c, int key, int value) {
     if (key == 15) {
         if (value != 0 && value != 1) return fail(c, PT_E_ARG, "culling walk: 0 = automatic, 1 = off");
         c->cons_off = value;
+        drop_graph(c);
+        return PT_OK;
+    }
+    if (key == 17) {
+        if (value != 0 && value != 256 && value != 512 && value != 768 && value != 1024)
+            return fail(c, PT_E_ARG, "wide walk workgroup: 256, 512, 768 or 1024 threads (0 = automatic)");
+        c->wide_threads = value;
         drop_graph(c);
         return PT_OK;
     }
@@ -2270,7 +2163,6 @@ static int launch_frames(const pt_ctx* c, int n_frames) {
 // gains (+7%).
 static bool cons_walk_on(const pt_ctx* c) {
     if (!c->walk_nested || c->cons_off || c->counting) return false;
-    if (!PT_WALK_SINKS) return true;
     const size_t mw = (size_t)(c->minw ? c->minw : 7);
     const auto blocks = [mw](size_t b) { return b ? std::min(mw, (size_t)(160 * 1024) / b) : mw; };
     return blocks(c->lds_bytes_sk) >= blocks(c->lds_bytes);
@@ -2280,7 +2172,11 @@ static bool cons_walk_on(const pt_ctx* c) {
 // (a nested tree), it lies inside the scene half of the exact-reciprocal guard (otherwise no
 // lane could use it), tuning key 16 leaves it on, nothing is counted, and the occupancy is
 // the automatic 6 waves per SIMD (the wide instantiations').
-constexpr int kWideTop = 512;   // wide records staged in LDS (24 KiB per 256-thread block)
+constexpr int kWideTopMax = 1 << 14;   // wide records staged in LDS: what the block's LDS share holds
+#ifndef PT_WIDE_THREADS
+#define PT_WIDE_THREADS 256
+#endif
+constexpr int kWideThreadsAuto = PT_WIDE_THREADS;   // threads per block of the wide walk (tuning key 17)
 static bool wide_walk_on(const pt_ctx* c) {
     return c->wide_ok && c->scene_fast && !c->wide_off && !c->counting && (c->minw == 0 || c->minw == 6);
 }
@@ -2444,10 +2340,13 @@ static int enqueue_render(pt_ctx* c, int frame_first, int n_frames, int acc_firs
     {
         // persistent grid: enough resident waves to fill every SIMD; surplus blocks find the
         // queue empty and exit.  Never more blocks than 8x8 tiles (64 lanes per tile).
-        size_t lds = use_lds ? ((PT_WALK_SINKS && p.cons_walk) ? c->lds_bytes_sk : c->lds_bytes) : 0;
+        size_t lds = use_lds ? (p.cons_walk ? c->lds_bytes_sk : c->lds_bytes) : 0;
         unsigned tiles = (unsigned)(((p.W + 7) / 8) * ((c->rows_local + 7) / 8));
         unsigned items = tiles * (unsigned)((n_frames + p.group - 1) / p.group);   // 64-lane items
-        const int nt = (variant == 0 && use_lds) ? lds_threads(c, lds) : 256;
+        // the wide walk's workgroup: wider ones share one LDS copy of more top records
+        // (tuning key 17); raysPerPixel > 1 keeps 256 threads
+        const int wide_nt = (use_wide && p.rpp == 1) ? (c->wide_threads ? c->wide_threads : kWideThreadsAuto) : 256;
+        const int nt = (variant == 0 && use_lds) ? lds_threads(c, lds) : (use_wide ? wide_nt : 256);
         const unsigned wpb = (unsigned)nt / 64u;                                    // waves per block
         unsigned blocks = std::min<unsigned>(c->persist_blocks * 256u / (unsigned)nt,
                                              std::max(1u, (items + wpb - 1) / wpb));
@@ -2462,9 +2361,11 @@ static int enqueue_render(pt_ctx* c, int frame_first, int n_frames, int acc_firs
         // materials + spheres beside the top nodes when they are small (<= 4 KiB)
         const size_t shade_bytes = (size_t)(3 * c->n_mats + 2 * c->n_spheres) * sizeof(float4);
         p.shade_lds = shade_bytes <= 4096;
-        if (use_wide)   // top records: 48 B each, within what mw blocks per CU leave beside the shading records
-            p.wide_top = (int)std::min<size_t>({(size_t)c->n_wide, (size_t)kWideTop,
-                                                ((size_t)160 * 1024 / (size_t)mw - (p.shade_lds ? shade_bytes : 0) - 256) / 48});
+        if (use_wide) {   // top records: 48 B each, within the block's share of the CU's LDS
+            const size_t blocks_cu = wide_nt == 1024 ? 1 : (size_t)(6 * 256 / wide_nt);
+            p.wide_top = (int)std::min<size_t>({(size_t)c->n_wide, (size_t)kWideTopMax,
+                                                ((size_t)160 * 1024 / blocks_cu - (p.shade_lds ? shade_bytes : 0) - 256) / 48});
+        }
         const size_t top_lds = use_wide ? (size_t)p.wide_top * 3 * sizeof(float4) + (p.shade_lds ? shade_bytes : 0)
                                         : (size_t)p.n_top * 2 * sizeof(float4) + (p.shade_lds ? shade_bytes : 0);
 #define PT_LAUNCH_SM(L, M)                                                                                \
@@ -2483,10 +2384,16 @@ static int enqueue_render(pt_ctx* c, int frame_first, int n_frames, int acc_firs
         // lds_threads: LDS scene, variant 0, one ray per pixel; the register budget of the
         // waves that are resident (6, 6, 4 per SIMD), not of 7
         if (use_wide) {
+#define PT_LAUNCH_WIDE_G(NT, MW)                                                                              \
+    if (p.rgb) hipLaunchKernelGGL((k_render_sm<false, false, MW, false, true, false, NT, true>), grid, dim3(NT), top_lds, rs, p); \
+    else hipLaunchKernelGGL((k_render_sm<false, false, MW, false, false, false, NT, true>), grid, dim3(NT), top_lds, rs, p);
             if (p.rgb && p.rpp > 1) hipLaunchKernelGGL((k_render_sm<false, false, 6, true, true, false, 256, true>), grid, dim3(256), top_lds, rs, p);
-            else if (p.rgb) hipLaunchKernelGGL((k_render_sm<false, false, 6, false, true, false, 256, true>), grid, dim3(256), top_lds, rs, p);
             else if (p.rpp > 1) hipLaunchKernelGGL((k_render_sm<false, false, 6, true, false, false, 256, true>), grid, dim3(256), top_lds, rs, p);
-            else hipLaunchKernelGGL((k_render_sm<false, false, 6, false, false, false, 256, true>), grid, dim3(256), top_lds, rs, p);
+            else if (nt == 512) { PT_LAUNCH_WIDE_G(512, 6) }
+            else if (nt == 768) { PT_LAUNCH_WIDE_G(768, 6) }
+            else if (nt == 1024) { PT_LAUNCH_WIDE_G(1024, 4) }
+            else { PT_LAUNCH_WIDE_G(256, 6) }
+#undef PT_LAUNCH_WIDE_G
         } else if (nt > 256) {
             if (nt == 512) { PT_LAUNCH_WIDE(512, 6) }
             else if (nt == 768) { PT_LAUNCH_WIDE(768, 6) }
@@ -2731,7 +2638,7 @@ int pt__scene_replicate_layout(pt_ctx* dst, const pt_ctx* src, void* dptr[10], c
     const size_t nm = 3 * (size_t)std::max(src->n_mats, 1), ns = 2 * (size_t)std::max(src->n_spheres, 1);
     const size_t nw = 16 * (size_t)src->walk_np, nk = src->d_walk_sk ? 18 * (size_t)src->walk_np : 0;
     const size_t ni = src->wide_ok ? (size_t)src->n_wide : 0;   // the wide walk's arrays (pt_wide.h)
-    const size_t sz[10] = {nd, nt, nm, ns, nw, nk, 4 * ni, 2 * ni, ni ? nd : 0, 8 * ni};
+    const size_t sz[10] = {nd, nt, nm, ns, nw, nk, kWideStride * ni, 2 * ni, ni ? nd : 0, 8 * ni};
     float4** mine[10] = {&dst->d_nodes, &dst->d_tris, &dst->d_mats, &dst->d_spheres, &dst->d_walk_lds, &dst->d_walk_sk,
                          &dst->d_wrec, &dst->d_wlbox, &dst->d_nodesw, &dst->d_trisw};
     const float4* theirs[10] = {src->d_nodes, src->d_tris, src->d_mats, src->d_spheres, src->d_walk_lds, src->d_walk_sk,
@@ -2764,6 +2671,16 @@ int pt__scene_replicate_layout(pt_ctx* dst, const pt_ctx* src, void* dptr[10], c
     // failed broadcast or copy must not leave a context rendering from uninitialised memory
     dst->scene_ok = false;
     return PT_OK;
+}
+
+// ACES epilogue of n RGBA32F pixels on a caller's stream (pt_group's gathered frame; the
+// same k_aces as pt_read_rgba8_aces and pt_present_*).  Internal, not part of the public ABI.
+int pt__aces_launch(const void* src, void* dst, long long n, void* stream) {
+    if (!src || !dst || n < 0) return PT_E_ARG;
+    if (n == 0) return PT_OK;
+    hipLaunchKernelGGL(k_aces, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream,
+                       (const float4*)src, (uchar4*)dst, n);
+    return hipGetLastError() == hipSuccess ? PT_OK : PT_E_HIP;
 }
 
 int pt__scene_set_ready(pt_ctx* c, int ready) {

@@ -123,6 +123,9 @@ def lib():
             "pt_group_upload_scene": (ip, [vp, _F, ip, _F, ip, _F, ip, _F, ip]),
             "pt_group_gather_rgba32f": (ip, [vp, vp, C.c_size_t, ip]),
             "pt_group_stats": (ip, [vp, C.POINTER(C.c_double), C.POINTER(C.c_size_t)]),
+            "pt_group_gather_rgba8_aces": (ip, [vp, vp, C.c_size_t, ip]),
+            "pt_group_present_begin": (ip, [vp, ip]),
+            "pt_group_present_end": (ip, [vp, ip, C.POINTER(C.POINTER(C.c_ubyte))]),
             "pt_gather_rgba32f": (ip, [C.POINTER(vp), ip, vp, C.c_size_t, ip]),
             "pt_viewer_create": (ip, [vp, ip, C.POINTER(vp)]),
             "pt_viewer_destroy": (None, [vp]),
@@ -547,6 +550,26 @@ class Group:
         out = np.zeros((self.H, self.W, 4), np.float32)
         self._check(lib().pt_group_gather_rgba32f(self.h, out.ctypes.data, nbytes, 0))
         return out
+
+    def gather_rgba8(self, device_ptr=None):
+        """The gathered frame through the ACES view (H, W, 4) uint8: to host, or into root-device
+        memory at device_ptr (returns None)."""
+        nbytes = self.W * self.H * 4
+        if device_ptr is not None:
+            self._check(lib().pt_group_gather_rgba8_aces(self.h, C.c_void_p(device_ptr), nbytes, 1))
+            return None
+        out = np.zeros((self.H, self.W, 4), np.uint8)
+        self._check(lib().pt_group_gather_rgba8_aces(self.h, out.ctypes.data, nbytes, 0))
+        return out
+
+    def present_begin(self, buf):
+        self._check(lib().pt_group_present_begin(self.h, int(buf)))
+
+    def present_end(self, buf, copy=True):
+        p = C.POINTER(C.c_ubyte)()
+        self._check(lib().pt_group_present_end(self.h, int(buf), C.byref(p)))
+        arr = np.ctypeslib.as_array(p, shape=(self.H, self.W, 4))
+        return arr.copy() if copy else arr
 
     def stats(self):
         ms, b = C.c_double(), C.c_size_t()

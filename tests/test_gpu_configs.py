@@ -6,8 +6,9 @@ SURVEY.md §8(d) C3-C5 and the reference's own shipped scenes:
   * C4 shape: the Sponza-style stand-in at 1920x1080 split over 8 row-interleaved rank
     contexts (world = 8) on one device, assembled as the 8-GPU run's gather assembles it;
   * C3 at its full 1920x1080 size;
-  * the reference's scene_data/drift (11,846 triangles, 24 materials) and p (6,258) scenes,
-    which take the global-memory walk (tests/golden/ref_scenes.npz, made by make_golden.py).
+  * the reference's scene_data/drift (11,846 triangles, 24 materials), p and p2 (6,258 each)
+    scenes, which take the global-memory walk (tests/golden/ref_scenes.npz, made by
+    make_golden.py).
 Full-size frames are checked at oracle-rendered sample pixels plus every pixel of the first
 and last rows (computeShader.c:505-554 per pixel); small ones in full.  No tolerance.
 """
@@ -35,7 +36,7 @@ def sample_xy(W, Hh, n, seed):
 @pytest.fixture(scope="module")
 def ref_scenes():
     z = np.load(os.path.join(GOLDEN, "ref_scenes.npz"))
-    return {k: H.scene_from_arrays(z[k + "_tris"], z[k + "_mats"]) for k in ("drift", "p")}
+    return {k: H.scene_from_arrays(z[k + "_tris"], z[k + "_mats"]) for k in ("drift", "p", "p2")}
 
 
 @pytest.fixture(scope="module")
@@ -109,7 +110,7 @@ def test_c3_full_size_sampled(bunny_scene):
     assert_bitwise(got[ys, xs], want, "C3 1080p samples")
 
 
-@pytest.mark.parametrize("name", ["drift", "p"])
+@pytest.mark.parametrize("name", ["drift", "p", "p2"])
 @pytest.mark.parametrize("variant", [0, 3])
 def test_reference_scenes_full_image(ref_scenes, name, variant):
     """The reference's own scenes, whole image, 4 frames, 8 bounces, frame offset 11 on a
@@ -128,7 +129,7 @@ def test_reference_scenes_full_image(ref_scenes, name, variant):
     assert_bitwise(got, want, "%s, variant %d" % (name, variant))
 
 
-@pytest.mark.parametrize("name", ["drift", "p"])
+@pytest.mark.parametrize("name", ["drift", "p", "p2"])
 def test_reference_scenes_full_hd_sampled(ref_scenes, name):
     """The reference's scenes at 1920x1080, 2 frames, sampled, and their reference-semantics
     work counts at a small size."""

@@ -105,3 +105,50 @@ def test_group_gather_time_excludes_renders(cornell_scene):
     for t in trs:
         t.close()
     assert render_ms > 5.0 and ms < 0.5 * render_ms, (ms, render_ms)
+
+
+@pytest.mark.parametrize("world", [1, 3, 8])
+def test_group_gather_aces(cornell_scene, world):
+    """pt_group_gather_rgba8_aces: the gathered frame through the reference's ACES view
+    (screenQuadFrag.c:12-33) on the root device, byte-equal to the host ACES of the oracle's
+    frame, to host memory and to device memory."""
+    import torch
+    W, Hh = 72, 45
+    want = O.aces_rgba8(O.render(cornell_scene, W, Hh, max_bounce=8, n_frames=3))
+    g, trs = split_render(cornell_scene, W, Hh, world, 3, order=list(range(world))[::-1])
+    got = g.gather_rgba8()
+    out = torch.zeros((Hh, W, 4), dtype=torch.uint8, device="cuda:0")
+    torch.cuda.synchronize()
+    g.gather_rgba8(device_ptr=out.data_ptr())
+    dev = out.cpu().numpy()
+    g.close()
+    for t in trs:
+        t.close()
+    assert np.array_equal(got, want) and np.array_equal(dev, want)
+    assert np.all(got[..., 3] == 255)
+
+
+def test_group_present_pipelined(cornell_scene):
+    """pt_group_present_begin / _end with renders queued behind them: frame f shown while f+1
+    and f+2 render (three buffers), each byte-equal to the ACES view of the oracle's
+    accumulation after that frame."""
+    W, Hh, world, n = 64, 40, 3, 6
+    trs = [H.PathTracer(W, Hh, max_bounce=8, rank=r, world=world) for r in range(world)]
+    g = H.Group(trs)
+    g.upload(cornell_scene)
+    shown = {}
+    for f in range(1, n + 1):
+        for t in trs:
+            t.render_async(f, 1, 0 if f == 1 else 1)
+        g.present_begin(f % 3)
+        if f >= 3:
+            shown[f - 2] = g.present_end((f - 2) % 3)
+    for f in (n - 1, n):
+        shown[f] = g.present_end(f % 3)
+    g.close()
+    for t in trs:
+        t.close()
+    acc = np.zeros((Hh, W, 4), np.float32)
+    for f in range(1, n + 1):
+        acc = O.render(cornell_scene, W, Hh, max_bounce=8, frame_first=f, n_frames=1, acc_first=int(f > 1), accum=acc)
+        assert np.array_equal(shown[f], O.aces_rgba8(acc)), f
