@@ -664,17 +664,20 @@ __device__ __forceinline__ void trav_walk(const SceneView& S, f3 o, f3 d, f3 rd,
 // position.  Lanes inside the exact-reciprocal guard only; their leaf boxes are re-tested
 // exactly in the leaf phase before a triangle may move t.  The first `wtop` records sit in
 // LDS as three planes (q0 at [i], q1 at [wtop + i], q2 at [2 wtop + i]).
+// (measured, same-process A/B on the C3 / C4 stand-ins: stack depth 3 and three record visits
+// per yield check with packed 48-B records +3.5% / +3.9% over depth 2, two visits, 64-B
+// stride; each alone +0.5 / +2.6% (depth), +1.3 / -0.2% (unroll), +0.5 / +0.3% (stride))
 #ifndef PT_WIDE_STACK
-#define PT_WIDE_STACK 2
+#define PT_WIDE_STACK 3
 #endif
 constexpr int kWideStack = PT_WIDE_STACK;
 // float4 per device record: the three quads of pt_wide.h packed (48 B) or on a 64-B stride
 #ifndef PT_WIDE_STRIDE
-#define PT_WIDE_STRIDE 4
+#define PT_WIDE_STRIDE 3
 #endif
 constexpr int kWideStride = PT_WIDE_STRIDE;
 #ifndef PT_WIDE_UNROLL
-#define PT_WIDE_UNROLL 2
+#define PT_WIDE_UNROLL 3
 #endif
 __device__ __forceinline__ void wrec_at(const SceneView& S, int n, float4& q0, float4& q1, float4& q2) {
     if (n < S.wtop) {
@@ -1377,6 +1380,7 @@ struct pt_ctx {
     float wide_cw[3] = {0, 0, 0};
     int wide_off = 0;               // tuning key 16: 1 = the binary global walk
     int wide_threads = 0;           // tuning key 17: threads per block of the wide walk (0 = automatic)
+    int overlap_bpc = 0;            // tuning key 18: render blocks per CU of overlapped short launches (0 = all)
     unsigned long long* d_counters = nullptr;
     unsigned int* d_work = nullptr;
     int* d_frame = nullptr;                      // progressive graph frame counter
@@ -1973,6 +1977,11 @@ int pt_set_tuning(pt_ctx* c, int key, int value) {
         drop_graph(c);
         return PT_OK;
     }
+    if (key == 18) {
+        if (value < 0 || value > 8) return fail(c, PT_E_ARG, "overlapped render blocks per CU must be 1..8 (0 = all)");
+        c->overlap_bpc = value;
+        return PT_OK;
+    }
     if (key == 17) {
         if (value != 0 && value != 256 && value != 512 && value != 768 && value != 1024)
             return fail(c, PT_E_ARG, "wide walk workgroup: 256, 512, 768 or 1024 threads (0 = automatic)");
@@ -2350,6 +2359,10 @@ static int enqueue_render(pt_ctx* c, int frame_first, int n_frames, int acc_firs
         const unsigned wpb = (unsigned)nt / 64u;                                    // waves per block
         unsigned blocks = std::min<unsigned>(c->persist_blocks * 256u / (unsigned)nt,
                                              std::max(1u, (items + wpb - 1) / wpb));
+        // overlapped short renders (tuning key 18): at most this many 256-thread blocks per CU,
+        // so the accumulate pass of the previous render finds free slots beside the next one
+        if (overlap && c->overlap_bpc > 0)
+            blocks = std::min<unsigned>(blocks, std::max(1u, (unsigned)(c->overlap_bpc * c->n_cu * 256 / nt)));
         dim3 grid(blocks);
         // occupancy: 7 waves/SIMD for LDS scenes (72 VGPRs, a few spilled: +0.8% on C2 over
         // 6, which was +5% over 5; 8 spills 20+ and loses 7%), 6 for global-memory scenes (7
@@ -2363,8 +2376,9 @@ static int enqueue_render(pt_ctx* c, int frame_first, int n_frames, int acc_firs
         p.shade_lds = shade_bytes <= 4096;
         if (use_wide) {   // top records: 48 B each, within the block's share of the CU's LDS
             const size_t blocks_cu = wide_nt == 1024 ? 1 : (size_t)(6 * 256 / wide_nt);
+            // (1 KiB below the even share: the allocation granule must not cost a block per CU)
             p.wide_top = (int)std::min<size_t>({(size_t)c->n_wide, (size_t)kWideTopMax,
-                                                ((size_t)160 * 1024 / blocks_cu - (p.shade_lds ? shade_bytes : 0) - 256) / 48});
+                                                ((size_t)160 * 1024 / blocks_cu - (p.shade_lds ? shade_bytes : 0) - 1024) / 48});
         }
         const size_t top_lds = use_wide ? (size_t)p.wide_top * 3 * sizeof(float4) + (p.shade_lds ? shade_bytes : 0)
                                         : (size_t)p.n_top * 2 * sizeof(float4) + (p.shade_lds ? shade_bytes : 0);

@@ -152,3 +152,27 @@ def test_group_present_pipelined(cornell_scene):
     for f in range(1, n + 1):
         acc = O.render(cornell_scene, W, Hh, max_bounce=8, frame_first=f, n_frames=1, acc_first=int(f > 1), accum=acc)
         assert np.array_equal(shown[f], O.aces_rgba8(acc)), f
+
+
+@pytest.mark.skipif(__import__("torch").cuda.device_count() < 2, reason="needs two GPUs")
+@pytest.mark.parametrize("world", [3, 5])
+def test_group_across_two_devices(cornell_scene, world):
+    """Contexts spread unevenly over two devices (so the device with more contexts has several
+    slots and the other padded ones): the cross-device branches -- ncclBroadcast of the scene,
+    the on-device copies to a device's other contexts, ncclGather of the row blocks and the
+    block table -- assemble the oracle's frame bit for bit."""
+    W, Hh = 80, 53
+    want = O.render(cornell_scene, W, Hh, max_bounce=8, n_frames=3)
+    trs = [H.PathTracer(W, Hh, max_bounce=8, rank=r, world=world, device=0 if r % 3 == 0 else 1)
+           for r in range(world)]
+    g = H.Group(trs)
+    g.upload(cornell_scene)
+    for t in trs:
+        t.render_async(1, 3, 0)
+    got = g.gather()
+    aces = g.gather_rgba8()
+    g.close()
+    for t in trs:
+        t.close()
+    assert_bitwise(got, want, "world %d over two devices" % world)
+    assert np.array_equal(aces, O.aces_rgba8(want))
