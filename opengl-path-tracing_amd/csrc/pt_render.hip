@@ -1293,23 +1293,45 @@ __global__ __launch_bounds__(1024) void k_tile_order(unsigned* __restrict__ cost
 // Running mean of the frame-split mode (:548-551): per local pixel, the launch's frames in
 // order from the per-frame colours the render kernel stored -- the same accumulate() the
 // lane applies in registers otherwise.  Pixels outside the dispatch footprint are skipped.
+// Each thread takes kAccumPix pixels a block-width apart (coalesced), their loads issued
+// together: beside a running render this pass gets a few block slots per CU, and with one
+// pixel per thread it was latency-bound (about 100 us for a 1080p frame against 15 us alone).
+#ifndef PT_ACCUM_PIX
+#define PT_ACCUM_PIX 4
+#endif
+constexpr int kAccumPix = PT_ACCUM_PIX;
 __global__ __launch_bounds__(256) void k_accum_frames(KParams p) {
     resolve_frames(p);
     // the render that used these queue heads has ended (this pass runs after it): ready them
     // for the slot's next render, which waits for this pass (no fill dispatch per launch)
     if (p.reset_work && blockIdx.x == 0 && threadIdx.x == 0) *p.reset_work = 0u;
     const long long n = (long long)p.rows_local * p.W;
-    const long long idx = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-    if (idx >= n) return;
-    const int crow = (int)(idx / p.W), cx = (int)(idx - (long long)crow * p.W);
-    if (cx >= p.x_limit || p.row0 + crow * p.row_stride >= p.y_limit) return;
-    float4 acc = p.acc_first ? p.accum[idx] : make_float4(0, 0, 0, 0);
-    const float* src = p.rgb + 3 * idx;
-    for (int k = 0; k < p.n_frames; k++) {
-        const f3 v = nt_load3(src + 3 * (size_t)k * (size_t)n);
-        acc = accumulate(acc, v, p.frame_first + k, k > 0 || p.acc_first == 1);
+    const long long base = (long long)blockIdx.x * blockDim.x * kAccumPix + threadIdx.x;
+    long long idx[kAccumPix];
+    bool on[kAccumPix];
+    float4 acc[kAccumPix];
+#pragma unroll
+    for (int j = 0; j < kAccumPix; j++) {
+        idx[j] = base + (long long)j * blockDim.x;
+        on[j] = idx[j] < n;
+        if (on[j]) {
+            const int crow = (int)(idx[j] / p.W), cx = (int)(idx[j] - (long long)crow * p.W);
+            on[j] = cx < p.x_limit && p.row0 + crow * p.row_stride < p.y_limit;
+        }
+        acc[j] = (on[j] && p.acc_first) ? p.accum[idx[j]] : make_float4(0, 0, 0, 0);
     }
-    p.accum[idx] = acc;
+    for (int k = 0; k < p.n_frames; k++) {
+        f3 v[kAccumPix];
+#pragma unroll
+        for (int j = 0; j < kAccumPix; j++)
+            v[j] = on[j] ? nt_load3(p.rgb + 3 * ((size_t)k * (size_t)n + (size_t)idx[j])) : mk(0, 0, 0);
+#pragma unroll
+        for (int j = 0; j < kAccumPix; j++)
+            acc[j] = accumulate(acc[j], v[j], p.frame_first + k, k > 0 || p.acc_first == 1);
+    }
+#pragma unroll
+    for (int j = 0; j < kAccumPix; j++)
+        if (on[j]) p.accum[idx[j]] = acc[j];
 }
 
 // ACES film tonemap epilogue (screenQuadFrag.c:12-26) -> RGBA8, alpha 255.
@@ -1380,7 +1402,7 @@ struct pt_ctx {
     float wide_cw[3] = {0, 0, 0};
     int wide_off = 0;               // tuning key 16: 1 = the binary global walk
     int wide_threads = 0;           // tuning key 17: threads per block of the wide walk (0 = automatic)
-    int overlap_bpc = 0;            // tuning key 18: render blocks per CU of overlapped short launches (0 = all)
+    int overlap_bpc = 0;            // tuning key 18: render blocks per CU of overlapped short launches (0 = automatic)
     unsigned long long* d_counters = nullptr;
     unsigned int* d_work = nullptr;
     int* d_frame = nullptr;                      // progressive graph frame counter
@@ -1978,7 +2000,7 @@ int pt_set_tuning(pt_ctx* c, int key, int value) {
         return PT_OK;
     }
     if (key == 18) {
-        if (value < 0 || value > 8) return fail(c, PT_E_ARG, "overlapped render blocks per CU must be 1..8 (0 = all)");
+        if (value < 0 || value > 8) return fail(c, PT_E_ARG, "overlapped render blocks per CU must be 1..8 (0 = automatic)");
         c->overlap_bpc = value;
         return PT_OK;
     }
@@ -2359,15 +2381,21 @@ static int enqueue_render(pt_ctx* c, int frame_first, int n_frames, int acc_firs
         const unsigned wpb = (unsigned)nt / 64u;                                    // waves per block
         unsigned blocks = std::min<unsigned>(c->persist_blocks * 256u / (unsigned)nt,
                                              std::max(1u, (items + wpb - 1) / wpb));
-        // overlapped short renders (tuning key 18): at most this many 256-thread blocks per CU,
-        // so the accumulate pass of the previous render finds free slots beside the next one
-        if (overlap && c->overlap_bpc > 0)
-            blocks = std::min<unsigned>(blocks, std::max(1u, (unsigned)(c->overlap_bpc * c->n_cu * 256 / nt)));
         dim3 grid(blocks);
         // occupancy: 7 waves/SIMD for LDS scenes (72 VGPRs, a few spilled: +0.8% on C2 over
         // 6, which was +5% over 5; 8 spills 20+ and loses 7%), 6 for global-memory scenes (7
         // leaves fewer top nodes per block in LDS: -6% on the C3 stand-in)
         const int mw = c->minw ? c->minw : (use_lds ? 7 : 6);
+        // Overlapped short renders (tuning key 18): at most this many 256-thread blocks per CU
+        // (automatic: one fewer than resident), so the accumulate pass and the ACES view of the
+        // previous render find free slots beside the next render instead of waiting for its
+        // blocks to retire.  1080p Cornell, one frame per dispatch (tools/interactive_fps.py):
+        // 0.534 -> 0.514 ms per frame, and 0.68 -> 0.55-0.58 with every frame shown
+        // (pt_present, lag 2); accumulate pass 243 -> 103 us.
+        if (overlap && nt == 256) {
+            const int bpc = c->overlap_bpc ? c->overlap_bpc : std::max(1, mw - 1);
+            grid.x = std::min<unsigned>(grid.x, (unsigned)(bpc * c->n_cu));
+        }
         // global scene: the top nodes staged per block, at most what mw blocks per CU fit in
         // its 160 KiB of LDS (the first K of the breadth-first numbering, any K <= n_top)
         if (mw > 6) p.n_top = std::min(c->n_top, 160 * 1024 / mw / 32 - 8);
@@ -2427,7 +2455,8 @@ static int enqueue_render(pt_ctx* c, int frame_first, int n_frames, int acc_firs
                 HIPCHK(c, hipStreamWaitEvent(c->stream, c->ev_rdone[sl], 0));
             }
             long long px = (long long)c->rows_local * p.W;
-            hipLaunchKernelGGL(k_accum_frames, dim3((unsigned)((px + 255) / 256)), dim3(256), 0, c->stream, p);
+            hipLaunchKernelGGL(k_accum_frames, dim3((unsigned)((px + 256 * kAccumPix - 1) / (256 * kAccumPix))), dim3(256),
+                               0, c->stream, p);
             if (overlap) {
                 HIPCHK(c, hipEventRecord(c->ev_adone[sl], c->stream));
                 c->adone_rec[sl] = true;
