@@ -2202,14 +2202,14 @@ static bool cons_walk_on(const pt_ctx* c) {
 // Whether a global-memory launch walks the wide tree: the scene has one
 // (a nested tree), it lies inside the scene half of the exact-reciprocal guard (otherwise no
 // lane could use it), tuning key 16 leaves it on, nothing is counted, and the occupancy is
-// the automatic 6 waves per SIMD (the wide instantiations').
+// one the wide instantiations cover (5-7 waves per SIMD; automatic 6).
 constexpr int kWideTopMax = 1 << 14;   // wide records staged in LDS: what the block's LDS share holds
 #ifndef PT_WIDE_THREADS
 #define PT_WIDE_THREADS 256
 #endif
 constexpr int kWideThreadsAuto = PT_WIDE_THREADS;   // threads per block of the wide walk (tuning key 17)
 static bool wide_walk_on(const pt_ctx* c) {
-    return c->wide_ok && c->scene_fast && !c->wide_off && !c->counting && (c->minw == 0 || c->minw == 6);
+    return c->wide_ok && c->scene_fast && !c->wide_off && !c->counting && c->minw != 8;
 }
 
 // Threads per workgroup of the state-machine kernel on an LDS-staged scene of `lds` bytes:
@@ -2434,6 +2434,8 @@ static int enqueue_render(pt_ctx* c, int frame_first, int n_frames, int acc_firs
             else if (nt == 512) { PT_LAUNCH_WIDE_G(512, 6) }
             else if (nt == 768) { PT_LAUNCH_WIDE_G(768, 6) }
             else if (nt == 1024) { PT_LAUNCH_WIDE_G(1024, 4) }
+            else if (mw == 5) { PT_LAUNCH_WIDE_G(256, 5) }
+            else if (mw == 7) { PT_LAUNCH_WIDE_G(256, 7) }
             else { PT_LAUNCH_WIDE_G(256, 6) }
 #undef PT_LAUNCH_WIDE_G
         } else if (nt > 256) {
