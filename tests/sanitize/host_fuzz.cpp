@@ -1,7 +1,8 @@
 // host_fuzz.cpp -- ASan + UBSan driver for the host-side ingest of the drop-in library
 // (csrc/pt_scene.cpp, csrc/pt_viewer.cpp): the OBJ/MTL loaders (reference and robust modes,
 // geometry_loader.h:15-142), the SAH builder (bvh.h:173-268), the culling-walk tree check and
-// the headless viewer controller (ogl_path_trace.h:258-364).  Test infrastructure only: built
+// the headless viewer controller (ogl_path_trace.h:258-364), and the wide tree builder of the
+// global-memory walk (pt_wide.cpp) on every accepted tree and the random ones.  Test infrastructure only: built
 // by tests/sanitize/Makefile with -fsanitize=address,undefined -fno-sanitize-recover, run by
 // tests/test_sanitize.py; any report aborts the process.
 //
@@ -13,6 +14,7 @@
 #include "../../include/pt_api.h"
 #include "../../include/pt_scene.h"
 #include "../../include/pt_viewer.h"
+#include "../../opengl-path-tracing_amd/csrc/pt_wide.h"
 
 #include <cmath>
 #include <cstdint>
@@ -82,7 +84,14 @@ void exercise(const char* obj, const char* mtl) {
                 std::vector<float> nodes((size_t)cnt[3] * 12), tris((size_t)cnt[0] * 16);
                 pt_scene_get_nodes(s, nodes.data(), cnt[3]);
                 pt_scene_get_tris(s, tris.data(), cnt[0]);
-                pt_bvh_culling_ok(nodes.data(), cnt[3]);
+                if (pt_bvh_culling_ok(nodes.data(), cnt[3]) == 1) {   // pt_upload_scene's wide build
+                    ptw::WideTree wt;
+                    std::vector<unsigned char> cop((size_t)cnt[3], 0);
+                    if (ptw::wide_build(nodes.data(), cnt[3], cop.data(), wt) != 0) {
+                        std::fprintf(stderr, "wide_build refused a nested tree\n");
+                        std::abort();
+                    }
+                }
                 std::vector<float> n2((size_t)(2 * cnt[0]) * 12);
                 int nn = 0;
                 pt_bvh_build(tris.data(), cnt[0], n2.data(), 2 * cnt[0], &nn);
@@ -162,6 +171,10 @@ void fuzz_nodes(int iters) {
         }
         const int r = pt_bvh_culling_ok(nd.data(), n);
         if (r != 0 && r != 1) std::abort();
+        if (r == 1) {
+            ptw::WideTree wt;
+            if (ptw::wide_build(nd.data(), n, nullptr, wt) != 0) std::abort();
+        }
     }
 }
 
