@@ -78,7 +78,13 @@ int wide_build(const float* bvh, int n_nodes, const unsigned char* leaf_cop, Wid
     std::vector<BN> bn(n_nodes);
     for (int i = 0; i < n_nodes; i++) {
         const float* nd = bvh + 12 * (size_t)i;
-        for (int q = 0; q < 3; q++) { bn[i].lo[q] = nd[q]; bn[i].hi[q] = nd[4 + q]; }
+        for (int q = 0; q < 3; q++) {
+            bn[i].lo[q] = nd[q];
+            bn[i].hi[q] = nd[4 + q];
+            // finite, ordered boxes only (the quantisation steps and codes are computed from
+            // them; the walk needs the scene half of the exact-reciprocal guard anyway)
+            if (!std::isfinite(nd[q]) || !std::isfinite(nd[4 + q]) || !(nd[q] <= nd[4 + q])) return -1;
+        }
         bn[i].leaf = nd[8] > -1.0f;
     }
     // children of the internal nodes reachable from the root (the threading of a nested tree:

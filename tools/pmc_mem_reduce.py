@@ -40,6 +40,8 @@ def reduce(root):
             d["l1_to_l2_read_frac"] = c["TCP_TCC_READ_REQ_sum"] / c["TCP_TOTAL_CACHE_ACCESSES_sum"]
         if "TD_TD_BUSY_sum" in c:
             d["td_cycles_per_vmem_instr"] = c["TD_TD_BUSY_sum"] / c["SQ_INSTS_VMEM_RD"]
+    if "TCC_HIT_sum" in c and "TCC_MISS_sum" in c:
+        d["l2_hit_rate"] = c["TCC_HIT_sum"] / max(c["TCC_HIT_sum"] + c["TCC_MISS_sum"], 1.0)
     return {"counters": c, "derived": d}
 
 
