@@ -311,12 +311,16 @@ int main(int argc, char** argv) {
     if (events) std::printf("replayed %s: %d frames, %d accumulation restarts\n", events, frames_run, resets);
 
     std::vector<unsigned char> rgba(4 * (size_t)W * H, 0);
-    for (int g = 0; g < nctx; g++) {     // the ACES view is tonemapped on each context's device
+    if (group) {      // the ACES view of the gathered frame, tonemapped on the root device
+        int grc = pt_group_gather_rgba8_aces(group, rgba.data(), rgba.size(), 0);
+        if (grc) { std::fprintf(stderr, "pt_group_gather_rgba8_aces: %s (%d)\n", pt_group_last_error(group), grc); return 1; }
+    }
+    for (int g = 0; g < nctx && !group; g++) {     // one context: its own ACES view and rows
         int rows = 0, r0 = 0, rs = 1;
         pt_rows(ctx[g], &rows, &r0, &rs);
         std::vector<unsigned char> part8(4 * (size_t)rows * W);
         CHECK(pt_read_rgba8_aces(ctx[g], part8.data(), part8.size()), ctx[g]);
-        if (!group) CHECK(pt_read_rgba32f(ctx[g], img.data(), img.size() * 4), ctx[g]);
+        CHECK(pt_read_rgba32f(ctx[g], img.data(), img.size() * 4), ctx[g]);
         for (int k = 0; k < rows; k++)
             std::memcpy(&rgba[4 * (size_t)(r0 + k * rs) * W], &part8[4 * (size_t)k * W], 4 * (size_t)W);
     }
