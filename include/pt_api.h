@@ -104,8 +104,12 @@ int pt_read_rgba8_aces(pt_ctx* ctx, unsigned char* host_dst, size_t bytes);
 /* Asynchronous presentation, for a loop that shows every frame (the reference draws each
  * frame's texture, ogl_path_trace.h:189-192).  pt_present_begin(buf) enqueues the ACES
  * epilogue of the image as of the renders issued so far, and its copy into the context's
- * pinned host buffer `buf` (0..3) on a separate copy stream; it does not wait, and later
- * renders overlap the copy.  pt_present_end(buf) waits for that copy and returns the
+ * pinned host buffer `buf` (0..3), both on the context stream; it does not wait, and later
+ * renders overlap the copy.  When the caller presented after its previous render too, the
+ * latest render's accumulate pass already wrote the view and only the copy is enqueued (a
+ * write through pt_accum_device's pointer or onto pt_stream's stream must therefore come
+ * after those calls, not before with a pointer kept from earlier).
+ * pt_present_end(buf) waits for that copy and returns the
  * rows_local * width RGBA8 pixels (same bytes as pt_read_rgba8_aces), valid until the next
  * pt_present_begin on `buf` or pt_destroy.  Showing frame f-2 while frames f-1 and f render
  * (three buffers in rotation) keeps two renders in flight, as the render-only loop does.

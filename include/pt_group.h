@@ -58,8 +58,8 @@ int pt_group_gather_rgba8_aces(pt_group* g, unsigned char* dst, size_t bytes, in
 
 /* Pipelined presentation (the multi-GPU pt_present_begin / pt_present_end): begin enqueues the
  * gather and the ACES epilogue of the frame as every context's stream has it now, then a copy
- * into pinned host buffer `buf` (0..3) on a separate stream, and returns at once; renders
- * queued afterwards wait only for the row packing.  end waits for that copy and returns the
+ * into pinned host buffer `buf` (0..3) behind it on the root's group stream, and returns at
+ * once; renders queued afterwards wait only for the row packing.  end waits for that copy and returns the
  * pinned pixels (valid until the buffer is begun again).  The gather time (pt_group_stats)
  * is that of the last gather begun. */
 int pt_group_present_begin(pt_group* g, int buf);

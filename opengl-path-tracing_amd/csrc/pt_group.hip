@@ -66,12 +66,11 @@ struct pt_group {
     std::vector<hipEvent_t> packed_ev;      // per device: its contexts' rows are packed
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     // pipelined ACES presentation (pt_group_present_*): per buffer an RGBA8 frame on the root
-    // device, its pinned host copy and events, and one copy stream
+    // device, its pinned host copy and the copy's event (on the root's group stream)
     uchar4* present_dev[kGroupPresentBufs] = {};
     unsigned char* present_host[kGroupPresentBufs] = {};
-    hipEvent_t ev_tonemap[kGroupPresentBufs] = {}, ev_copied[kGroupPresentBufs] = {};
+    hipEvent_t ev_copied[kGroupPresentBufs] = {};
     bool present_pending[kGroupPresentBufs] = {};
-    hipStream_t cstream = nullptr;
     uchar4* rgba8 = nullptr;                // root: the ACES frame of pt_group_gather_rgba8_aces
     double last_ms = 0.0;
     std::string err;
@@ -117,14 +116,11 @@ void pt_group_destroy(pt_group* g) {
     }
     if (!g->devs.empty()) {
         (void)hipSetDevice(g->devs[0]);
-        if (g->cstream) (void)hipStreamSynchronize(g->cstream);
         for (int b = 0; b < kGroupPresentBufs; b++) {
             (void)hipFree(g->present_dev[b]);
             if (g->present_host[b]) (void)hipHostFree(g->present_host[b]);
-            if (g->ev_tonemap[b]) (void)hipEventDestroy(g->ev_tonemap[b]);
             if (g->ev_copied[b]) (void)hipEventDestroy(g->ev_copied[b]);
         }
-        if (g->cstream) (void)hipStreamDestroy(g->cstream);
         (void)hipFree(g->rgba8);
         (void)hipFree(g->recv);
         (void)hipFree(g->frame);
@@ -371,12 +367,10 @@ int pt_group_present_begin(pt_group* g, int buf) {
     if (buf < 0 || buf >= kGroupPresentBufs) return gfail(g, PT_E_ARG, "present buffer must be 0..3");
     const long long n = (long long)g->W * (long long)g->H;
     GHIP(g, hipSetDevice(g->devs[0]));
-    if (!g->cstream) GHIP(g, hipStreamCreateWithFlags(&g->cstream, hipStreamNonBlocking));
     if (!g->present_dev[buf]) {
         GHIP(g, hipMalloc(&g->present_dev[buf], std::max<long long>(n, 1) * sizeof(uchar4)));
         GHIP(g, hipHostMalloc((void**)&g->present_host[buf], std::max<long long>(n, 1) * sizeof(uchar4),
                               hipHostMallocDefault));
-        GHIP(g, hipEventCreateWithFlags(&g->ev_tonemap[buf], hipEventDisableTiming));
         GHIP(g, hipEventCreateWithFlags(&g->ev_copied[buf], hipEventDisableTiming));
     }
     // a buffer begun again before its end: its previous copy must land first
@@ -387,11 +381,12 @@ int pt_group_present_begin(pt_group* g, int buf) {
     GHIP(g, hipSetDevice(g->devs[0]));
     rc = pt__aces_launch(g->frame, g->present_dev[buf], n, g->stream[0]);
     if (rc) return gfail(g, rc, "k_aces launch");
-    GHIP(g, hipEventRecord(g->ev_tonemap[buf], g->stream[0]));
-    GHIP(g, hipStreamWaitEvent(g->cstream, g->ev_tonemap[buf], 0));
+    // the copy on the root's group stream, behind the ACES pass: a copy stream waiting on an
+    // event started each copy ~150 us late (pt_present_begin); the contexts'
+    // renders wait only for the next gather's pack, not for this copy
     if (n) GHIP(g, hipMemcpyAsync(g->present_host[buf], g->present_dev[buf], (size_t)n * 4, hipMemcpyDeviceToHost,
-                                  g->cstream));
-    GHIP(g, hipEventRecord(g->ev_copied[buf], g->cstream));
+                                  g->stream[0]));
+    GHIP(g, hipEventRecord(g->ev_copied[buf], g->stream[0]));
     g->present_pending[buf] = true;
     return PT_OK;
 }

@@ -83,6 +83,7 @@ struct KParams {
     // group = n_frames and rgb = null: the lane owns all frames and accumulates in registers.
     int group;
     float* rgb;                    // 3 floats per (frame, pixel)
+    uchar4* aces_out;              // k_accum_frames: also the ACES view of the new image (or null)
     float rW, rH;                  // RN(1/W), RN(1/H) (host IEEE division) for the camera ray
     float fW, fH;                  // W, H as binary32 (kernel arguments: uniform, no VGPR)
     unsigned grp_magic;            // ceil(2^32 / n_groups) when item * n_groups < 2^32 for every item, else 0
@@ -1290,6 +1291,19 @@ __global__ __launch_bounds__(1024) void k_tile_order(unsigned* __restrict__ cost
     for (int t = tid; t < n_tiles; t += 1024) cost[t] = 0u;
 }
 
+// ACES film tonemap (screenQuadFrag.c:12-26) of one pixel -> RGBA8, alpha 255.
+__device__ __forceinline__ uchar4 aces_px(float4 v) {
+    float c[3] = {v.x, v.y, v.z};
+    unsigned char o[3];
+    for (int k = 0; k < 3; k++) {
+        float x = c[k];
+        float tm = (x * (2.51f * x + 0.03f)) / (x * (2.43f * x + 0.59f) + 0.14f);
+        tm = tm < 0.0f ? 0.0f : (tm > 1.0f ? 1.0f : tm);
+        if (!(tm == tm)) tm = 0.0f;
+        o[k] = (unsigned char)(int)(tm * 255.0f + 0.5f);
+    }
+    return make_uchar4(o[0], o[1], o[2], 255);
+}
 // Running mean of the frame-split mode (:548-551): per local pixel, the launch's frames in
 // order from the per-frame colours the render kernel stored -- the same accumulate() the
 // lane applies in registers otherwise.  Pixels outside the dispatch footprint are skipped.
@@ -1305,17 +1319,19 @@ __global__ __launch_bounds__(256) void k_accum_frames(KParams p) {
     // the render that used these queue heads has ended (this pass runs after it): ready them
     // for the slot's next render, which waits for this pass (no fill dispatch per launch)
     if (p.reset_work && blockIdx.x == 0 && threadIdx.x == 0) *p.reset_work = 0u;
-    const long long n = (long long)p.rows_local * p.W;
-    const long long base = (long long)blockIdx.x * blockDim.x * kAccumPix + threadIdx.x;
-    long long idx[kAccumPix];
+    // rows_local * W < 2^31 (pt_create), and the grid covers n rounded up to a block's pixels:
+    // 32-bit pixel indices
+    const unsigned n = (unsigned)p.rows_local * (unsigned)p.W;
+    const unsigned base = blockIdx.x * blockDim.x * kAccumPix + threadIdx.x;
+    unsigned idx[kAccumPix];
     bool on[kAccumPix];
     float4 acc[kAccumPix];
 #pragma unroll
     for (int j = 0; j < kAccumPix; j++) {
-        idx[j] = base + (long long)j * blockDim.x;
+        idx[j] = base + (unsigned)j * blockDim.x;
         on[j] = idx[j] < n;
         if (on[j]) {
-            const int crow = (int)(idx[j] / p.W), cx = (int)(idx[j] - (long long)crow * p.W);
+            const int crow = (int)(idx[j] / (unsigned)p.W), cx = (int)(idx[j] - (unsigned)crow * (unsigned)p.W);
             on[j] = cx < p.x_limit && p.row0 + crow * p.row_stride < p.y_limit;
         }
         acc[j] = (on[j] && p.acc_first) ? p.accum[idx[j]] : make_float4(0, 0, 0, 0);
@@ -1332,24 +1348,36 @@ __global__ __launch_bounds__(256) void k_accum_frames(KParams p) {
 #pragma unroll
     for (int j = 0; j < kAccumPix; j++)
         if (on[j]) p.accum[idx[j]] = acc[j];
+    // the ACES view of the new image for pt_present_begin (pixels outside the dispatch
+    // footprint keep their old value): the same aces_px of the same values as k_aces
+    if (p.aces_out) {
+#pragma unroll
+        for (int j = 0; j < kAccumPix; j++)
+            if (idx[j] < n) p.aces_out[idx[j]] = aces_px(on[j] ? acc[j] : p.accum[idx[j]]);
+    }
 }
 
-// ACES film tonemap epilogue (screenQuadFrag.c:12-26) -> RGBA8, alpha 255.
+// ACES film tonemap epilogue (aces_px) of n pixels.  Each thread
+// takes kAcesPix pixels a block-width apart (coalesced), their loads issued together: the pass
+// runs beside the next render with few free slots per CU, latency-bound (as k_accum_frames).
+#ifndef PT_ACES_PIX
+#define PT_ACES_PIX 4
+#endif
+constexpr int kAcesPix = PT_ACES_PIX;
 __global__ __launch_bounds__(256) void k_aces(const float4* __restrict__ src, uchar4* __restrict__ dst,
                                               long long n) {
-    long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
-    float4 v = src[i];
-    float c[3] = {v.x, v.y, v.z};
-    unsigned char o[3];
-    for (int k = 0; k < 3; k++) {
-        float x = c[k];
-        float tm = (x * (2.51f * x + 0.03f)) / (x * (2.43f * x + 0.59f) + 0.14f);
-        tm = tm < 0.0f ? 0.0f : (tm > 1.0f ? 1.0f : tm);
-        if (!(tm == tm)) tm = 0.0f;
-        o[k] = (unsigned char)(int)(tm * 255.0f + 0.5f);
+    const long long base = (long long)blockIdx.x * blockDim.x * kAcesPix + threadIdx.x;
+    float4 v[kAcesPix];
+#pragma unroll
+    for (int j = 0; j < kAcesPix; j++) {
+        const long long i = base + (long long)j * blockDim.x;
+        v[j] = i < n ? src[i] : make_float4(0, 0, 0, 0);
     }
-    dst[i] = make_uchar4(o[0], o[1], o[2], 255);
+#pragma unroll
+    for (int j = 0; j < kAcesPix; j++) {
+        const long long i = base + (long long)j * blockDim.x;
+        if (i < n) dst[i] = aces_px(v[j]);
+    }
 }
 
 }  // namespace
@@ -1379,6 +1407,7 @@ constexpr int kMaxSlots = 4, kAutoSlots = 2;
 constexpr size_t kQueueSet = kQueueStride;   // unsigned per queue head
 
 constexpr int kPresentBufs = 4;   // pt_present_begin buffers
+
 struct pt_ctx {
     pt_config cfg{};
     int rows_local = 0;
@@ -1467,13 +1496,17 @@ struct pt_ctx {
     float last_ms = 0.0f;
     unsigned long long last_counts[16] = {0};
     bool count_pending = false;
-    // asynchronous presentation (pt_present_begin / _end): per buffer a device RGBA8 image, a
-    // pinned host copy, its events, and one copy stream shared by the buffers
-    uchar4* present_dev[kPresentBufs] = {};
+    // asynchronous presentation (pt_present_begin / _end): per buffer a pinned host image and
+    // its copy event; the device view is rgba8 (one, as the copies and the passes that write
+    // it are ordered on the context stream)
     unsigned char* present_host[kPresentBufs] = {};
-    hipEvent_t ev_tonemap[kPresentBufs] = {}, ev_copied[kPresentBufs] = {};
+    hipEvent_t ev_copied[kPresentBufs] = {};
     bool present_pending[kPresentBufs] = {};
-    hipStream_t cstream = nullptr;
+    // The accumulate pass writes the ACES view into rgba8 beside the running mean when the
+    // caller presented after the previous render (aces_fuse, from `presented`); stage_ok: rgba8
+    // holds the view of the current image (set by such a pass, cleared by anything that may
+    // change the image or rgba8 afterwards).
+    bool presented = false, aces_fuse = false, stage_ok = false;
     std::string err;
 };
 
@@ -1590,14 +1623,11 @@ void pt_destroy(pt_ctx* c) {
         if (c->ev_adone[i]) (void)hipEventDestroy(c->ev_adone[i]);
     }
     if (c->ev_fence) (void)hipEventDestroy(c->ev_fence);
-    if (c->cstream) (void)hipStreamSynchronize(c->cstream);
+    if (c->stream) (void)hipStreamSynchronize(c->stream);
     for (int b = 0; b < kPresentBufs; b++) {
-        (void)hipFree(c->present_dev[b]);
         if (c->present_host[b]) (void)hipHostFree(c->present_host[b]);
-        if (c->ev_tonemap[b]) (void)hipEventDestroy(c->ev_tonemap[b]);
         if (c->ev_copied[b]) (void)hipEventDestroy(c->ev_copied[b]);
     }
-    if (c->cstream) (void)hipStreamDestroy(c->cstream);
     for (auto& pr : c->ev_pending) { c->ev_free.push_back(pr.first); c->ev_free.push_back(pr.second); }
     for (hipEvent_t e : c->ev_free) (void)hipEventDestroy(e);
     if (c->stream) (void)hipStreamDestroy(c->stream);
@@ -2233,6 +2263,7 @@ static int lds_threads(const pt_ctx* c, size_t lds) {
 // `frame_dev` the frame range is read on the device (progressive graph replay).
 static int enqueue_render(pt_ctx* c, int frame_first, int n_frames, int acc_first, const int* frame_dev,
                           int frame_offset, bool force_sort = false) {
+    c->stage_ok = false;    // this launch changes the image: rgba8 holds its view only if written below
     KParams p;
     std::memset(&p, 0, sizeof(p));
     p.sc.nodes = c->d_nodes;
@@ -2457,6 +2488,10 @@ static int enqueue_render(pt_ctx* c, int frame_first, int n_frames, int acc_firs
                 HIPCHK(c, hipStreamWaitEvent(c->stream, c->ev_rdone[sl], 0));
             }
             long long px = (long long)c->rows_local * p.W;
+            // a presenting caller's view of the new image, written by the same pass (not inside
+            // a captured graph: its replays are not followed by pt_present_begin's check)
+            p.aces_out = (c->aces_fuse && !frame_dev) ? c->rgba8 : nullptr;
+            c->stage_ok = p.aces_out != nullptr;
             hipLaunchKernelGGL(k_accum_frames, dim3((unsigned)((px + 256 * kAccumPix - 1) / (256 * kAccumPix))), dim3(256),
                                0, c->stream, p);
             if (overlap) {
@@ -2536,6 +2571,10 @@ int pt_render_async(pt_ctx* c, int frame_first, int n_frames, int acc_first) {
     int rc = take_events(c, ev);
     if (rc) return rc;
     HIPCHK(c, hipEventRecord(ev[0], c->stream));
+    // a caller that presented after its previous render gets the ACES view from this render's
+    // accumulate pass (pt_present_begin then only copies it)
+    c->aces_fuse = c->presented;
+    c->presented = false;
     rc = enqueue_frames(c, frame_first, n_frames, acc_first, nullptr, 0);
     if (rc) return rc;
     HIPCHK(c, hipEventRecord(ev[1], c->stream));
@@ -2559,6 +2598,7 @@ static void drop_graph(pt_ctx* c) {
 
 int pt_progressive_setup(pt_ctx* c, int frames_per_launch, int launches_per_replay) {
     if (!c) return PT_E_ARG;
+    c->stage_ok = false;
     if (!c->scene_ok) return fail(c, PT_E_STATE, "pt_progressive_setup before pt_upload_scene");
     if (frames_per_launch <= 0 || launches_per_replay <= 0) return fail(c, PT_E_ARG, "counts must be > 0");
     if (c->counting) return fail(c, PT_E_STATE, "counting is not supported in graph replay");
@@ -2604,6 +2644,7 @@ int pt_progressive_reset(pt_ctx* c, int next_frame) {
 
 int pt_progressive_run(pt_ctx* c, int replays) {
     if (!c) return PT_E_ARG;
+    c->stage_ok = false;
     if (!c->graph_exec) return fail(c, PT_E_STATE, "pt_progressive_setup first");
     if (replays <= 0) return fail(c, PT_E_ARG, "replays must be > 0");
     HIPCHK(c, hipSetDevice(c->cfg.device));
@@ -2723,7 +2764,7 @@ int pt__scene_replicate_layout(pt_ctx* dst, const pt_ctx* src, void* dptr[10], c
 int pt__aces_launch(const void* src, void* dst, long long n, void* stream) {
     if (!src || !dst || n < 0) return PT_E_ARG;
     if (n == 0) return PT_OK;
-    hipLaunchKernelGGL(k_aces, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream,
+    hipLaunchKernelGGL(k_aces, dim3((unsigned)((n + 256 * kAcesPix - 1) / (256 * kAcesPix))), dim3(256), 0, (hipStream_t)stream,
                        (const float4*)src, (uchar4*)dst, n);
     return hipGetLastError() == hipSuccess ? PT_OK : PT_E_HIP;
 }
@@ -2746,6 +2787,7 @@ int pt_read_rgba32f(pt_ctx* c, float* dst, size_t bytes) {
 
 int pt_write_rgba32f(pt_ctx* c, const float* src, size_t bytes) {
     if (!c || !src) return PT_E_ARG;
+    c->stage_ok = false;
     size_t need = (size_t)c->rows_local * c->cfg.width * sizeof(float4);
     if (bytes < need) return fail(c, PT_E_ARG, "source too small");
     HIPCHK(c, hipSetDevice(c->cfg.device));
@@ -2760,7 +2802,7 @@ int pt_read_rgba8_aces(pt_ctx* c, unsigned char* dst, size_t bytes) {
     if (bytes < (size_t)n * 4) return fail(c, PT_E_ARG, "destination too small");
     if (n == 0) return PT_OK;
     HIPCHK(c, hipSetDevice(c->cfg.device));
-    hipLaunchKernelGGL(k_aces, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, c->stream, c->accum, c->rgba8, n);
+    hipLaunchKernelGGL(k_aces, dim3((unsigned)((n + 256 * kAcesPix - 1) / (256 * kAcesPix))), dim3(256), 0, c->stream, c->accum, c->rgba8, n);
     HIPCHK(c, hipGetLastError());
     HIPCHK(c, hipStreamSynchronize(c->stream));
     HIPCHK(c, hipMemcpy(dst, c->rgba8, (size_t)n * 4, hipMemcpyDeviceToHost));
@@ -2778,28 +2820,30 @@ int pt_present_begin(pt_ctx* c, int buf) {
     if (buf < 0 || buf >= kPresentBufs) return fail(c, PT_E_ARG, "present buffer must be 0..3");
     const long long n = (long long)c->rows_local * c->cfg.width;
     HIPCHK(c, hipSetDevice(c->cfg.device));
-    if (!c->cstream) HIPCHK(c, hipStreamCreateWithFlags(&c->cstream, hipStreamNonBlocking));
-    if (!c->present_dev[buf]) {
-        HIPCHK(c, hipMalloc(&c->present_dev[buf], std::max<long long>(n, 1) * sizeof(uchar4)));
+    if (!c->present_host[buf]) {
         HIPCHK(c, hipHostMalloc((void**)&c->present_host[buf], std::max<long long>(n, 1) * sizeof(uchar4),
                                 hipHostMallocDefault));
-        HIPCHK(c, hipEventCreateWithFlags(&c->ev_tonemap[buf], hipEventDisableTiming));
         HIPCHK(c, hipEventCreateWithFlags(&c->ev_copied[buf], hipEventDisableTiming));
     }
     // a buffer begun again before its end: its previous copy must land first
     if (c->present_pending[buf]) HIPCHK(c, hipEventSynchronize(c->ev_copied[buf]));
     c->present_pending[buf] = false;
-    if (n > 0) {
-        hipLaunchKernelGGL(k_aces, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, c->stream, c->accum,
-                           c->present_dev[buf], n);
+    // the view of the current image: written by the last render's accumulate pass when the
+    // caller presented after the render before it (stage_ok), else the ACES pass here
+    if (n > 0 && !c->stage_ok) {
+        hipLaunchKernelGGL(k_aces, dim3((unsigned)((n + 256 * kAcesPix - 1) / (256 * kAcesPix))), dim3(256), 0,
+                           c->stream, c->accum, c->rgba8, n);
         HIPCHK(c, hipGetLastError());
     }
-    HIPCHK(c, hipEventRecord(c->ev_tonemap[buf], c->stream));
-    HIPCHK(c, hipStreamWaitEvent(c->cstream, c->ev_tonemap[buf], 0));
+    c->stage_ok = false;
+    c->presented = true;
+    // the copy on the context stream itself: a copy stream waiting on an event started each
+    // copy about 150 us after the view was ready (one-frame loop with lag 2: 0.578 -> 0.537
+    // ms per frame); the next render's accumulate pass, which rewrites the view, follows it
     if (n > 0)
-        HIPCHK(c, hipMemcpyAsync(c->present_host[buf], c->present_dev[buf], (size_t)n * sizeof(uchar4),
-                                 hipMemcpyDeviceToHost, c->cstream));
-    HIPCHK(c, hipEventRecord(c->ev_copied[buf], c->cstream));
+        HIPCHK(c, hipMemcpyAsync(c->present_host[buf], c->rgba8, (size_t)n * sizeof(uchar4), hipMemcpyDeviceToHost,
+                                 c->stream));
+    HIPCHK(c, hipEventRecord(c->ev_copied[buf], c->stream));
     c->present_pending[buf] = true;
     return PT_OK;
 }
@@ -2817,6 +2861,7 @@ int pt_present_end(pt_ctx* c, int buf, const unsigned char** pixels) {
 
 int pt_accum_device(pt_ctx* c, void** ptr, size_t* bytes) {
     if (!c) return PT_E_ARG;
+    c->stage_ok = false;   // the caller may write the image through this pointer
     if (ptr) *ptr = c->accum;
     if (bytes) *bytes = (size_t)c->rows_local * c->cfg.width * sizeof(float4);
     return PT_OK;
@@ -2841,6 +2886,7 @@ int pt_timing(pt_ctx* c, double* total_ms, int* n, int reset) {
 
 int pt_stream(pt_ctx* c, void** s) {
     if (!c || !s) return PT_E_ARG;
+    c->stage_ok = false;   // ... or queue work on this stream that does
     *s = (void*)c->stream;
     return PT_OK;
 }

@@ -258,3 +258,41 @@ def test_present_pipelined(cornell_scene, world, lag):
         with pytest.raises(H.PTError):
             pt.present_begin(4)
         pt.close()
+
+
+def test_present_fused_view_tracks_the_image(cornell_scene):
+    """After a present, the next render's accumulate pass writes the ACES view itself and
+    pt_present_begin only copies it.  Whatever changes the image in between -- a write of the
+    accumulation, a long render, a progressive graph replay, a render with presentation paused --
+    must still show the view of the current image, byte-equal to the host ACES."""
+    W, Hh = 64, 36
+    acc = lambda n: O.render(cornell_scene, W, Hh, max_bounce=6, n_frames=n)
+    pt = H.PathTracer(W, Hh, max_bounce=6)
+    pt.upload(cornell_scene)
+    pt.render_async(1, 1, 0)
+    pt.present_begin(0)
+    pt.render_async(2, 1, 1)                       # fused: the view comes from this pass
+    pt.present_begin(1)
+    assert np.array_equal(pt.present_end(1), H.aces_rgba8_host(acc(2)))
+    pt.render_async(3, 1, 1)                       # fused, then the image is overwritten
+    seed = np.random.default_rng(3).random((Hh, W, 4), dtype=np.float32) * 2.0
+    pt.write_rgba32f(seed)
+    pt.present_begin(0)
+    assert np.array_equal(pt.present_end(0), H.aces_rgba8_host(seed))
+    pt.render_async(1, 1, 0)
+    pt.present_begin(0)
+    pt.render_async(2, 40, 1)                      # a long launch after a present
+    pt.present_begin(1)
+    assert np.array_equal(pt.present_end(1), H.aces_rgba8_host(acc(41)))
+    pt.render_async(42, 1, 1)
+    pt.render_async(43, 1, 1)                      # no present after 42: 43 is not fused
+    pt.present_begin(2)
+    pt.present_begin(3)                            # twice, nothing rendered between
+    want = H.aces_rgba8_host(acc(43))
+    assert np.array_equal(pt.present_end(2), want) and np.array_equal(pt.present_end(3), want)
+    pt.progressive_setup(2, 1)                     # graph replays after a present
+    pt.progressive_reset(44)
+    pt.progressive_run(1)
+    pt.present_begin(0)
+    assert np.array_equal(pt.present_end(0), H.aces_rgba8_host(acc(45)))
+    pt.close()
