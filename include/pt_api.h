@@ -112,7 +112,7 @@ int pt_read_rgba8_aces(pt_ctx* ctx, unsigned char* host_dst, size_t bytes);
  * pt_present_end(buf) waits for that copy and returns the
  * rows_local * width RGBA8 pixels (same bytes as pt_read_rgba8_aces), valid until the next
  * pt_present_begin on `buf` or pt_destroy.  Showing frame f-2 while frames f-1 and f render
- * (three buffers in rotation) keeps two renders in flight, as the render-only loop does.
+ * (three buffers in rotation) keeps renders in flight, as the render-only loop does.
  * A buffer begun again before its end first waits for its previous copy.
  * PT_E_STATE: end without a begin. */
 int pt_present_begin(pt_ctx* ctx, int buf);
@@ -174,7 +174,7 @@ int pt_set_kernel(pt_ctx* ctx, int variant);
  *         A render whose per-frame colours (12 B per pixel-frame) exceed it -- or whose
  *         32-bit work-queue ids would overflow -- runs as back-to-back launches, the first
  *         with the caller's accumulate flag and the rest accumulating: the same image.
- * key 9 = overlapped short launches: render slots 2..4, 1 = off, 0 = automatic (2).  Renders
+ * key 9 = overlapped short launches: render slots 2..4, 1 = off, 0 = automatic (3).  Renders
  *         of at most 16 frames (the reference's one dispatch per displayed frame) run their
  *         render kernel on one of these extra streams, so the next render fills the CUs that
  *         this one's launch tail frees; the running mean is still applied on the context's

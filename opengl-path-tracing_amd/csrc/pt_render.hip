@@ -1400,10 +1400,13 @@ constexpr size_t kLdsSceneSmall = 48 * 1024;  // staged by 256-thread workgroups
 constexpr int kTopNodes = 768;
 // overlapped short launches: render slots (tuning key 9).  A slot's scratch is reused only
 // after the accumulate pass that read it.  Measured on 1080p Cornell one-frame launches (ms per
-// frame): 1 slot (no overlap) 0.80, 2 slots 0.60, 3 slots 0.62, 4 slots 0.66 -- more slots
-// put more renders in flight, whose blocks then hold the CUs longer before the accumulate
-// passes (and with them the slots) come free.
-constexpr int kMaxSlots = 4, kAutoSlots = 2;
+// frame, round 3): 1 slot (no overlap) 0.80, 2 slots 0.60, 3 slots 0.62, 4 slots 0.66 -- more
+// slots put more renders in flight, whose blocks then held the CUs before the accumulate passes
+// (and with them the slots) came free.  With the blocks-per-CU cap (key 18) and presentation
+// on the context stream (round 4; render only / every frame shown at lag 2): 2 slots at 6
+// blocks per CU 0.516 / 0.522-0.547, 3 slots at 6 0.509 / 0.525, 3 at 5 0.505 / 0.527, 3 at 4
+// 0.503 / 0.532, 4 at 4-5 0.615 / 0.59.
+constexpr int kMaxSlots = 4, kAutoSlots = 3;
 constexpr size_t kQueueSet = kQueueStride;   // unsigned per queue head
 
 constexpr int kPresentBufs = 4;   // pt_present_begin buffers
@@ -2418,13 +2421,13 @@ static int enqueue_render(pt_ctx* c, int frame_first, int n_frames, int acc_firs
         // leaves fewer top nodes per block in LDS: -6% on the C3 stand-in)
         const int mw = c->minw ? c->minw : (use_lds ? 7 : 6);
         // Overlapped short renders (tuning key 18): at most this many 256-thread blocks per CU
-        // (automatic: one fewer than resident), so the accumulate pass and the ACES view of the
+        // (automatic: one fewer than resident, two fewer with 3+ render slots), so the accumulate pass and the ACES view of the
         // previous render find free slots beside the next render instead of waiting for its
         // blocks to retire.  1080p Cornell, one frame per dispatch (tools/interactive_fps.py):
         // 0.534 -> 0.514 ms per frame, and 0.68 -> 0.55-0.58 with every frame shown
         // (pt_present, lag 2); accumulate pass 243 -> 103 us.
         if (overlap && nt == 256) {
-            const int bpc = c->overlap_bpc ? c->overlap_bpc : std::max(1, mw - 1);
+            const int bpc = c->overlap_bpc ? c->overlap_bpc : std::max(1, mw - (c->overlap_slots >= 3 ? 2 : 1));
             grid.x = std::min<unsigned>(grid.x, (unsigned)(bpc * c->n_cu));
         }
         // global scene: the top nodes staged per block, at most what mw blocks per CU fit in
@@ -2802,8 +2805,15 @@ int pt_read_rgba8_aces(pt_ctx* c, unsigned char* dst, size_t bytes) {
     if (bytes < (size_t)n * 4) return fail(c, PT_E_ARG, "destination too small");
     if (n == 0) return PT_OK;
     HIPCHK(c, hipSetDevice(c->cfg.device));
-    hipLaunchKernelGGL(k_aces, dim3((unsigned)((n + 256 * kAcesPix - 1) / (256 * kAcesPix))), dim3(256), 0, c->stream, c->accum, c->rgba8, n);
-    HIPCHK(c, hipGetLastError());
+    // the view the last render's accumulate pass wrote when the caller also read (or presented)
+    // after the render before it (pt_present_begin), else the ACES pass here
+    if (!c->stage_ok) {
+        hipLaunchKernelGGL(k_aces, dim3((unsigned)((n + 256 * kAcesPix - 1) / (256 * kAcesPix))), dim3(256), 0,
+                           c->stream, c->accum, c->rgba8, n);
+        HIPCHK(c, hipGetLastError());
+    }
+    c->stage_ok = true;     // rgba8 is the view of the current image
+    c->presented = true;
     HIPCHK(c, hipStreamSynchronize(c->stream));
     HIPCHK(c, hipMemcpy(dst, c->rgba8, (size_t)n * 4, hipMemcpyDeviceToHost));
     return PT_OK;
@@ -2835,7 +2845,7 @@ int pt_present_begin(pt_ctx* c, int buf) {
                            c->stream, c->accum, c->rgba8, n);
         HIPCHK(c, hipGetLastError());
     }
-    c->stage_ok = false;
+    c->stage_ok = true;     // rgba8 is the view of the current image
     c->presented = true;
     // the copy on the context stream itself: a copy stream waiting on an event started each
     // copy about 150 us after the view was ready (one-frame loop with lag 2: 0.578 -> 0.537
