@@ -296,3 +296,20 @@ def test_present_fused_view_tracks_the_image(cornell_scene):
     pt.present_begin(0)
     assert np.array_equal(pt.present_end(0), H.aces_rgba8_host(acc(45)))
     pt.close()
+
+
+def test_read_rgba8_fused_view(cornell_scene):
+    """pt_read_rgba8_aces after every render (the synchronous show-every-frame loop) takes the
+    view from the accumulate pass from the second frame on: byte-equal to the host ACES, also
+    when a present and a read follow the same render."""
+    W, Hh = 48, 30
+    pt = H.PathTracer(W, Hh, max_bounce=6)
+    pt.upload(cornell_scene)
+    for f in range(1, 5):
+        pt.render(f, 1, int(f > 1))
+        want = H.aces_rgba8_host(O.render(cornell_scene, W, Hh, max_bounce=6, n_frames=f))
+        assert np.array_equal(pt.read_rgba8(), want), f
+        pt.present_begin(f % 2)
+        assert np.array_equal(pt.present_end(f % 2), want), f
+        assert np.array_equal(pt.read_rgba8(), want), f
+    pt.close()
