@@ -1407,6 +1407,14 @@ constexpr int kTopNodes = 768;
 // blocks per CU 0.516 / 0.522-0.547, 3 slots at 6 0.509 / 0.525, 3 at 5 0.505 / 0.527, 3 at 4
 // 0.503 / 0.532, 4 at 4-5 0.615 / 0.59.
 constexpr int kMaxSlots = 4, kAutoSlots = 3;
+// Scratch ring of overlapped launches: each launch takes the next entry (colour scratch, queue
+// head, render / accumulate events) of a ring kRingMult times as long as the render streams, so
+// a render waits for the accumulate pass of the launch kRingMult * slots back, not of the one
+// that last used its stream (which the stream order already puts before it).
+#ifndef PT_RING_MULT
+#define PT_RING_MULT 2
+#endif
+constexpr int kRingMult = PT_RING_MULT, kRingMax = kRingMult * kMaxSlots;
 constexpr size_t kQueueSet = kQueueStride;   // unsigned per queue head
 
 constexpr int kPresentBufs = 4;   // pt_present_begin buffers
@@ -1477,14 +1485,15 @@ struct pt_ctx {
     // (created with the highest priority, so its small grid is dispatched as soon as render
     // blocks retire) in frame order
     hipStream_t rstream[kMaxSlots] = {};
-    float* slot_rgb[kMaxSlots] = {};
-    size_t slot_rgb_bytes[kMaxSlots] = {};
-    hipEvent_t ev_rdone[kMaxSlots] = {}, ev_adone[kMaxSlots] = {};
+    float* slot_rgb[kRingMax] = {};
+    size_t slot_rgb_bytes[kRingMax] = {};
+    hipEvent_t ev_rdone[kRingMax] = {}, ev_adone[kRingMax] = {};
     // main-stream fence an overlapped render waits for: recorded after every tile-order sort
     // and graph replay (the writers of tile_perm, which the render reads)
     hipEvent_t ev_fence = nullptr;
-    bool adone_rec[kMaxSlots] = {}, fence_rec = false;
+    bool adone_rec[kRingMax] = {}, fence_rec = false;
     int slot = 0;
+    int ring = 0;                   // next scratch-ring entry of an overlapped launch
     int overlap_slots = kAutoSlots;   // tuning key 9 (1 = one stream, no overlap)
     // frame-split scratch budget: a render needing more is issued as back-to-back launches
     // (tuning key 8; default min(32 GiB, a quarter of the device memory))
@@ -1581,7 +1590,7 @@ int pt_create(const pt_config* cfg, pt_ctx** out) {
     HIPCHK(c, hipMalloc(&c->d_counters, 16 * sizeof(unsigned long long)));
     // work-queue heads (kQueueStride apart): one for the main stream and
     // one per overlap slot
-    HIPCHK(c, hipMalloc(&c->d_work, kQueueSet * sizeof(unsigned) * (1 + kMaxSlots)));
+    HIPCHK(c, hipMalloc(&c->d_work, kQueueSet * sizeof(unsigned) * (1 + kRingMax)));
     int n_cu = 0;
     HIPCHK(c, hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, cfg->device));
     c->persist_blocks = (unsigned)std::max(1, n_cu) * 8u;   // 8 x 256 threads = 32 waves per CU
@@ -1619,9 +1628,11 @@ void pt_destroy(pt_ctx* c) {
     (void)hipFree(c->d_tile_cost);
     (void)hipFree(c->d_rgb);
     for (int i = 0; i < kMaxSlots; i++) {
-        (void)hipFree(c->slot_rgb[i]);
         if (c->rstream[i]) (void)hipStreamSynchronize(c->rstream[i]);
         if (c->rstream[i]) (void)hipStreamDestroy(c->rstream[i]);
+    }
+    for (int i = 0; i < kRingMax; i++) {
+        (void)hipFree(c->slot_rgb[i]);
         if (c->ev_rdone[i]) (void)hipEventDestroy(c->ev_rdone[i]);
         if (c->ev_adone[i]) (void)hipEventDestroy(c->ev_adone[i]);
     }
@@ -2024,6 +2035,7 @@ int pt_set_tuning(pt_ctx* c, int key, int value) {
         HIPCHK(c, hipStreamSynchronize(c->stream));
         c->overlap_slots = value ? value : kAutoSlots;
         c->slot = 0;
+        c->ring = 0;
         return PT_OK;
     }
     if (key == 15) {
@@ -2162,26 +2174,28 @@ static int ensure_rgb(pt_ctx* c, int n_frames) {
     return PT_OK;
 }
 
-// Scratch, stream and events of overlap slot `sl` (enqueue_render), created on first use.  The
-// slot's buffer may still be read by the accumulate pass of the last launch that used it, so
-// a reallocation first drains the main stream and the slot's render stream.
-static int ensure_slot(pt_ctx* c, int sl, int n_frames) {
-    if (!c->rstream[sl]) {
-        HIPCHK(c, hipStreamCreateWithFlags(&c->rstream[sl], hipStreamNonBlocking));
-        HIPCHK(c, hipEventCreateWithFlags(&c->ev_rdone[sl], hipEventDisableTiming));
-        HIPCHK(c, hipEventCreateWithFlags(&c->ev_adone[sl], hipEventDisableTiming));
-        // the slot's queue heads start at zero; afterwards each accumulate pass re-zeroes them
-        HIPCHK(c, hipMemset(c->d_work + kQueueSet * (1 + sl), 0, kQueueSet * sizeof(unsigned)));
+// Render stream `sl` and scratch-ring entry `e` of an overlapped launch (enqueue_render),
+// created on first use.  The entry's buffer may still be read by the accumulate pass of the
+// last launch that used it, on any render stream, so a reallocation first drains the main
+// stream (every accumulate pass) and the render streams.
+static int ensure_slot(pt_ctx* c, int sl, int e, int n_frames) {
+    if (!c->rstream[sl]) HIPCHK(c, hipStreamCreateWithFlags(&c->rstream[sl], hipStreamNonBlocking));
+    if (!c->ev_rdone[e]) {
+        HIPCHK(c, hipEventCreateWithFlags(&c->ev_rdone[e], hipEventDisableTiming));
+        HIPCHK(c, hipEventCreateWithFlags(&c->ev_adone[e], hipEventDisableTiming));
+        // the entry's queue heads start at zero; afterwards each accumulate pass re-zeroes them
+        HIPCHK(c, hipMemset(c->d_work + kQueueSet * (1 + e), 0, kQueueSet * sizeof(unsigned)));
     }
     const size_t need = (size_t)std::max(c->rows_local, 1) * (size_t)c->cfg.width * (size_t)n_frames * 3 * sizeof(float);
-    if (need <= c->slot_rgb_bytes[sl]) return PT_OK;
+    if (need <= c->slot_rgb_bytes[e]) return PT_OK;
     HIPCHK(c, hipStreamSynchronize(c->stream));
-    HIPCHK(c, hipStreamSynchronize(c->rstream[sl]));
-    (void)hipFree(c->slot_rgb[sl]);
-    c->slot_rgb[sl] = nullptr;
-    c->slot_rgb_bytes[sl] = 0;
-    HIPCHK(c, hipMalloc(&c->slot_rgb[sl], need));
-    c->slot_rgb_bytes[sl] = need;
+    for (int i = 0; i < kMaxSlots; i++)
+        if (c->rstream[i]) HIPCHK(c, hipStreamSynchronize(c->rstream[i]));
+    (void)hipFree(c->slot_rgb[e]);
+    c->slot_rgb[e] = nullptr;
+    c->slot_rgb_bytes[e] = 0;
+    HIPCHK(c, hipMalloc(&c->slot_rgb[e], need));
+    c->slot_rgb_bytes[e] = need;
     return PT_OK;
 }
 
@@ -2362,16 +2376,19 @@ static int enqueue_render(pt_ctx* c, int frame_first, int n_frames, int acc_firs
     const bool overlap = c->overlap_slots > 1 && !frame_dev && !c->counting && n_frames <= kShortLaunch &&
                          split_mode(c, n_frames, p.group);
     const int sl = c->slot;
+    const int ring = kRingMult * c->overlap_slots;
+    const int re = c->ring % ring;       // this launch's scratch-ring entry
     hipStream_t rs = c->stream;
     unsigned* work = c->d_work;
     if (overlap) {
-        int rc = ensure_slot(c, sl, n_frames);
+        int rc = ensure_slot(c, sl, re, n_frames);
         if (rc) return rc;
         rs = c->rstream[sl];
-        work = c->d_work + kQueueSet * (1 + sl);
-        p.rgb = c->slot_rgb[sl];
+        work = c->d_work + kQueueSet * (1 + re);
+        p.rgb = c->slot_rgb[re];
         p.work_counter = work;
         c->slot = (sl + 1) % c->overlap_slots;
+        c->ring = (re + 1) % ring;
     } else if (split_mode(c, n_frames, p.group)) {
         int rc = ensure_rgb(c, n_frames);
         if (rc) return rc;
@@ -2395,7 +2412,7 @@ static int enqueue_render(pt_ctx* c, int frame_first, int n_frames, int acc_firs
         std::memcpy(p.wide_cw, c->wide_cw, sizeof(p.wide_cw));
     }
     if (overlap) {
-        if (c->adone_rec[sl]) HIPCHK(c, hipStreamWaitEvent(rs, c->ev_adone[sl], 0));
+        if (c->adone_rec[re]) HIPCHK(c, hipStreamWaitEvent(rs, c->ev_adone[re], 0));
         if (c->fence_rec) HIPCHK(c, hipStreamWaitEvent(rs, c->ev_fence, 0));
     }
     // an overlap slot's heads were zeroed by the accumulate pass of its last render (or at
@@ -2487,8 +2504,8 @@ static int enqueue_render(pt_ctx* c, int frame_first, int n_frames, int acc_firs
         }
         if (p.rgb) {
             if (overlap) {
-                HIPCHK(c, hipEventRecord(c->ev_rdone[sl], rs));
-                HIPCHK(c, hipStreamWaitEvent(c->stream, c->ev_rdone[sl], 0));
+                HIPCHK(c, hipEventRecord(c->ev_rdone[re], rs));
+                HIPCHK(c, hipStreamWaitEvent(c->stream, c->ev_rdone[re], 0));
             }
             long long px = (long long)c->rows_local * p.W;
             // a presenting caller's view of the new image, written by the same pass (not inside
@@ -2498,8 +2515,8 @@ static int enqueue_render(pt_ctx* c, int frame_first, int n_frames, int acc_firs
             hipLaunchKernelGGL(k_accum_frames, dim3((unsigned)((px + 256 * kAccumPix - 1) / (256 * kAccumPix))), dim3(256),
                                0, c->stream, p);
             if (overlap) {
-                HIPCHK(c, hipEventRecord(c->ev_adone[sl], c->stream));
-                c->adone_rec[sl] = true;
+                HIPCHK(c, hipEventRecord(c->ev_adone[re], c->stream));
+                c->adone_rec[re] = true;
             }
         }
     }
