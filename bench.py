@@ -13,6 +13,9 @@ value = ray segments (calculateRayCollision calls, computeShader.c:450) of all r
 max-over-ranks wall time, in Mrays/s.  Segment counts come from an untimed counting pass
 over the same frames (reference traversal semantics; identical image).
 
+The default run (C2 on one GPU) also times the global-memory configs C3 and C4 (2 steps each)
+and reports them under "secondary", each with its own roofline.
+
 Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--config C2|C3|C4|C5]
 N>1:   python -m torch.distributed.run --nproc-per-node N bench.py --gpus N ...
 """
@@ -32,6 +35,9 @@ sys.path.insert(0, PKG)
 METRIC = "Mrays/sec + ms/frame @1920×1080, 8 bounces, 1/2/4/8 MI355X"
 HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
 N_SIMD = 1024           # 256 CUs x 4 SIMDs; a wave64 VALU instruction holds a SIMD-32 for 2 cycles
+N_CU = 256
+WAVES_PER_SIMD_PEAK = 8  # wave slots per SIMD (the occupancy peak)
+PMC_DIR = os.path.join(REPO, "profiles", "pmc")
 
 # scene, W, H, spp, bounces, frames per launch, graph launches/replay
 CONFIGS = {
@@ -76,11 +82,19 @@ def cpu_model():
     return "unknown"
 
 
+def pmc_path(config, world):
+    """The PMC summary bench.py reads for a workload: tools/pmc_traffic.py writes
+    profiles/pmc/<config>[_w<N>].json (per-rank share at N > 1) beside its per-round copy."""
+    return os.path.join(PMC_DIR, "%s%s.json" % (config, "" if world == 1 else "_w%d" % world))
+
+
 def pmc_for(traffic_json, lib_path, W, H, chunk, scene, world):
     """-> (PMC summary or None, why not, sha256 of the library).  The PMC figures count only
     for this exact build and workload: the pass records the sha256 of the library it
     profiled (tools/pmc_traffic.py), and a rebuilt kernel without a fresh pass gets frac =
-    null -- dividing an old instruction count by a new time would not be a roofline."""
+    null -- dividing an old instruction count by a new time would not be a roofline.  At
+    N > 1 the workload is one rank's share (rank 0 of the row split, frames per launch as
+    launched), so rank 0's line carries the roofline of its own share."""
     with open(lib_path, "rb") as fh:
         lib_sha = hashlib.sha256(fh.read()).hexdigest()
     try:
@@ -88,13 +102,241 @@ def pmc_for(traffic_json, lib_path, W, H, chunk, scene, world):
             tj = json.load(fh)
     except (OSError, ValueError) as e:
         return None, "no PMC pass (%s)" % e, lib_sha
-    if (tj.get("width"), tj.get("height"), tj.get("chunk"), tj.get("scene")) != (W, H, chunk, scene) or world != 1:
-        return None, "PMC pass is of another workload (%s %sx%s, %s frames per launch)" % (
-            tj.get("scene"), tj.get("width"), tj.get("height"), tj.get("chunk")), lib_sha
+    if (tj.get("width"), tj.get("height"), tj.get("chunk"), tj.get("scene"), tj.get("world", 1)) != (W, H, chunk, scene,
+                                                                                                      world):
+        return None, "PMC pass is of another workload (%s %sx%s, %s frames per launch, world %s)" % (
+            tj.get("scene"), tj.get("width"), tj.get("height"), tj.get("chunk"), tj.get("world", 1)), lib_sha
     if tj.get("lib_sha256") != lib_sha:
         return None, "PMC pass profiled another build (lib sha256 %s, this build %s)" % (
             str(tj.get("lib_sha256"))[:12], lib_sha[:12]), lib_sha
     return tj, None, lib_sha
+
+
+def roofline_from(pmc, stale, lib_sha, avg_launch_ms, n_launch, segments_per_launch, alg_bytes_per_launch):
+    """Roofline of the render launch from a PMC summary of the same build and workload.
+    Two issue-side bounds, both utilisations of a unit every CU has one of (per SIMD for VALU):
+      valu    achieved = SQ_INSTS_VALU per launch / live launch time; peak = 1024 SIMDs x clock / 2
+              (a wave64 VALU instruction holds a SIMD-32 for 2 cycles)
+      texture achieved = TD_TD_BUSY cycles per launch (summed over CUs) / live launch time;
+              peak = 256 CUs x clock (the texture-data unit that returns every vector-memory
+              load; the global-memory walk's scattered gathers keep it busy)
+    `bound` is the one with the larger fraction.  HBM stays a secondary field: the scene is
+    LDS / L2 / MALL-resident, and the algorithmic bytes are mostly LDS and
+    L1 reads.  Occupancy: resident waves per SIMD (SQ_WAVE_CYCLES is counted in quad-cycles on
+    gfx950) against the 8 wave slots."""
+    t = avg_launch_ms * 1e-3
+    hbm = {"algorithmic_gbs": round(alg_bytes_per_launch / t / 1e9, 1),
+           "algorithmic_frac": round(alg_bytes_per_launch / t / 1e9 / HBM_PEAK_GBS, 4),
+           "algorithmic_bytes_per_launch": int(alg_bytes_per_launch), "peak": HBM_PEAK_GBS, "unit": "GB/s"}
+    r = {"bound": None, "achieved": None, "peak": None, "unit": None, "frac": None, "traffic": None,
+         "avg_launch_ms": round(avg_launch_ms, 3), "n_launches": n_launch, "lib_sha256": lib_sha[:16]}
+    if stale:
+        r["pmc_stale"] = stale
+    if pmc is not None:
+        c = pmc["counters_per_launch"]
+        clk = pmc["clock_ghz"]
+        cands = {}
+        if c.get("SQ_INSTS_VALU"):
+            a = c["SQ_INSTS_VALU"] / t / 1e9
+            cands["valu"] = {"achieved": round(a, 2), "peak": round(N_SIMD * clk / 2.0, 2), "unit": "G wave-VALU instr/s",
+                             "per_segment": round(c["SQ_INSTS_VALU"] / segments_per_launch, 2)}
+        if c.get("TD_TD_BUSY_sum"):
+            a = c["TD_TD_BUSY_sum"] / t / 1e9
+            cands["texture"] = {"achieved": round(a, 2), "peak": round(N_CU * clk, 2), "unit": "G TD-busy cycles/s",
+                                "per_segment": round(c["TD_TD_BUSY_sum"] / segments_per_launch, 2)}
+        for k, v in cands.items():
+            v["frac"] = round(v["achieved"] / v["peak"], 4)
+        if cands:
+            b = max(cands, key=lambda k: cands[k]["frac"])
+            r.update(bound=b, achieved=cands[b]["achieved"], peak=cands[b]["peak"], unit=cands[b]["unit"],
+                     frac=cands[b]["frac"])
+            r["bounds"] = cands
+        r["clock_ghz_pmc"] = round(clk, 3)
+        if c.get("SQ_WAVE_CYCLES") and c.get("GRBM_GUI_ACTIVE"):
+            w = 4.0 * c["SQ_WAVE_CYCLES"] / (c["GRBM_GUI_ACTIVE"] / 8.0 * N_SIMD)
+            r["occupancy"] = {"waves_per_simd": round(w, 2), "peak": WAVES_PER_SIMD_PEAK,
+                              "frac": round(w / WAVES_PER_SIMD_PEAK, 4)}
+        if c.get("SQ_ACTIVE_INST_VALU"):
+            r["active_lanes_per_valu"] = round(c["SQ_THREAD_CYCLES_VALU"] / c["SQ_ACTIVE_INST_VALU"], 2)
+        mem = {}
+        if c.get("TCP_TOTAL_CACHE_ACCESSES_sum"):
+            mem["l1_accesses_per_segment"] = round(c["TCP_TOTAL_CACHE_ACCESSES_sum"] / segments_per_launch, 2)
+            mem["l1_to_l2_per_segment"] = round(c["TCP_TCC_READ_REQ_sum"] / segments_per_launch, 2)
+        if c.get("SQ_INSTS_VMEM_RD"):
+            mem["vmem_load_instr_per_segment"] = round(c["SQ_INSTS_VMEM_RD"] / segments_per_launch, 3)
+            if c.get("TD_TD_BUSY_sum"):
+                mem["td_cycles_per_vmem_instr"] = round(c["TD_TD_BUSY_sum"] / c["SQ_INSTS_VMEM_RD"], 1)
+        if c.get("TD_TC_STALL_sum") and c.get("TD_TD_BUSY_sum"):
+            mem["td_stalled_on_l1_frac"] = round(c["TD_TC_STALL_sum"] / c["TD_TD_BUSY_sum"], 3)
+        if c.get("TCC_HIT_sum") is not None and c.get("TCC_MISS_sum") is not None:
+            mem["l2_hit_rate"] = round(c["TCC_HIT_sum"] / max(c["TCC_HIT_sum"] + c["TCC_MISS_sum"], 1.0), 4)
+        if mem:
+            r["memory_pipe"] = mem
+        if pmc.get("hbm_bytes_per_launch"):
+            tb = pmc["hbm_bytes_per_launch"]
+            r["traffic"] = int(tb)
+            hbm.update(traffic_bytes_per_launch=int(tb), measured_gbs=round(tb / t / 1e9, 1),
+                       measured_frac=round(tb / t / 1e9 / HBM_PEAK_GBS, 4),
+                       traffic_over_algorithmic=round(tb / alg_bytes_per_launch, 2))
+        r["source"] = pmc.get("source")
+        if pmc.get("pmc_launch_ms"):   # the PMC pass's own launch time beside the live one
+            r["pmc_launch_ms"] = round(pmc["pmc_launch_ms"], 3)
+    r["hbm"] = hbm
+    r["basis"] = ("achieved = PMC count per launch (SQ_INSTS_VALU or TD_TD_BUSY_sum) / live avg launch time "
+                  "(HIP events on the render stream); peak = 1024 SIMDs x clock / 2 (VALU) or 256 CUs x clock "
+                  "(texture-data unit), clock held in the PMC pass; HBM kept as a secondary field")
+    return r
+
+
+def measure(cfg, args, ctx, steps, warmup, cold=True, W=None, H=None, spp=None, bounces=None, chunk=None,
+            dump=False):
+    """One configuration on this rank: scene (rank 0 builds it, N > 1 broadcasts), optional
+    cold first render, `warmup` untimed steps, `steps` timed steps (barrier + synchronize on
+    both sides, max over ranks), an untimed counting pass over the same frames, and the
+    roofline from the PMC summary of this build and per-rank workload."""
+    import torch
+    import pt_host
+    import pt_scenes
+    world, rank, device, distributed = ctx["world"], ctx["rank"], ctx["device"], ctx["distributed"]
+    dist, backend = ctx.get("dist"), args.dist_backend
+    scene, W0, H0, spp0, b0, chunk0, graph_launches = CONFIGS[cfg]
+    W, H, spp = W or W0, H or H0, spp or spp0
+    bounces = b0 if bounces is None else bounces
+    # frames per launch: the per-GPU share of the image shrinks with N, so launches get N times
+    # more frames, capped at spp (one launch tail per launch; measured: C2 on one GPU runs 2.5%
+    # faster as one 1024-frame launch than as 8 of 128, and a 1080p/8 share runs at the
+    # single-GPU rate with 1024-frame launches, 13% slower with 128).  The graph config (C5)
+    # keeps its captured launch shape.
+    if not chunk:
+        chunk = chunk0 * world if graph_launches == 0 else chunk0
+    chunk = min(chunk, spp)
+    coll_dev = "cuda" if backend == "nccl" else "cpu"
+
+    def barrier():
+        if distributed:
+            dist.barrier()
+
+    # the scene is generated, parsed and its BVH built once, on rank 0, then broadcast
+    # (pt_dist.broadcast_scene; RCCL for nccl) -- every rank renders the same arrays
+    sb = None
+    if rank == 0:
+        sb = pt_host.setupBuffers(*pt_scenes.write_scene(scene, os.path.join(REPO, "scenes")))
+    if distributed:
+        import pt_dist
+        sb = pt_dist.broadcast_scene(sb, device=coll_dev)
+    cold_ms = None
+    if cold and graph_launches == 0:
+        # cold first render: a fresh context right after pt_upload_scene (raster tile order
+        # until the probe launch's costs are sorted), after a tiny render on a throw-away
+        # context has loaded the code object -- what one render of a new scene costs
+        warm = pt_host.PathTracer(64, 32, max_bounce=bounces, device=device)
+        warm.upload(sb)
+        warm.render(1, 2, 0)
+        warm.close()
+        c0 = pt_host.PathTracer(W, H, max_bounce=bounces, display_mode=1, device=device, rank=rank, world=world)
+        c0.set_kernel(args.variant)
+        c0.upload(sb)
+        barrier()
+        tc = time.perf_counter()
+        for f0 in range(1, spp + 1, chunk):
+            c0.render_async(f0, min(chunk, spp - (f0 - 1)), 0 if f0 == 1 else 1)
+        c0.sync()
+        cold_ms = (time.perf_counter() - tc) * 1e3
+        c0.close()
+        if distributed:
+            t = torch.tensor([cold_ms], dtype=torch.float64, device=coll_dev)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            cold_ms = float(t.item())
+    pt = pt_host.PathTracer(W, H, max_bounce=bounces, display_mode=1, device=device, rank=rank, world=world)
+    pt.set_kernel(args.variant)
+    pt.upload(sb)
+    launches = [(f0, min(chunk, spp - (f0 - 1))) for f0 in range(1, spp + 1, chunk)]
+    use_graph = graph_launches > 0 and spp % (chunk * graph_launches) == 0
+    if use_graph:
+        pt.progressive_setup(chunk, graph_launches)
+        replays = spp // (chunk * graph_launches)
+
+    if distributed:
+        import pt_dist
+        rmax = pt_dist.rows_max(H, world)
+        send = torch.zeros((rmax, W, 4), dtype=torch.float32, device=coll_dev)
+        # the rows leave the render context by a device copy in both modes (the RCCL path's
+        # pt_copy_rows_device); the gloo rehearsal then stages them through host memory
+        dsend = send if coll_dev == "cuda" else torch.zeros((rmax, W, 4), dtype=torch.float32, device="cuda")
+
+    def step():
+        if use_graph:
+            pt.progressive_reset(1)
+            pt.progressive_run(replays, sync=False)
+        else:
+            for f0, n in launches:
+                pt.render_async(f0, n, 0 if f0 == 1 else 1)
+        pt.sync()
+        if distributed:
+            pt.copy_rows_device(dsend.data_ptr(), pt.rows_local * W * 16)
+            if backend != "nccl":
+                send.copy_(dsend)
+            img = pt_dist.gather_image(send, H, world)
+            if backend == "nccl":
+                torch.cuda.synchronize()
+            return img
+        return None
+
+    for _ in range(warmup):
+        step()
+    pt.timing(reset=True)
+    barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    img = None
+    for _ in range(steps):
+        img = step()
+    torch.cuda.synchronize()
+    barrier()
+    dt = time.perf_counter() - t0
+    kern_ms, n_launch = pt.timing(reset=True)
+    if use_graph:
+        n_launch = steps * replays * graph_launches      # events bracket whole replays
+    if distributed:
+        t = torch.tensor([dt], dtype=torch.float64, device=coll_dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
+
+    # untimed counting pass over the same frames: exact reference-semantics work counts
+    pt.set_counting(True)
+    tot = dict(segments=0, node_visits=0, tri_tests=0, sphere_tests=0, hits=0)
+    alg_bytes = 0
+    for f0, n in launches:
+        pt.render(f0, n, 0 if f0 == 1 else 1)
+        _, cnt = pt.stats()
+        for k in tot:
+            tot[k] += cnt[k]
+        alg_bytes += algorithmic_bytes(cnt, pt.rows_local * W, f0 == 1)
+    pt.set_counting(False)
+    seg_rank = float(tot["segments"])
+    if distributed:
+        v = torch.tensor([tot["segments"], alg_bytes], dtype=torch.float64, device=coll_dev)
+        dist.all_reduce(v, op=dist.ReduceOp.SUM)
+        seg_all = float(v[0])
+    else:
+        seg_all = seg_rank
+    avg_launch_ms = kern_ms / max(n_launch, 1)
+    pmc_json = args.traffic_json if (args.traffic_json and cfg == args.config) else pmc_path(cfg, world)
+    pmc, stale, lib_sha = pmc_for(pmc_json, pt_host.LIB_PATH, W, H, chunk, scene, world)
+    roofline = roofline_from(pmc, stale, lib_sha, avg_launch_ms, n_launch, seg_rank / len(launches),
+                             alg_bytes / len(launches))
+    frame = None
+    if dump and rank == 0:
+        frame = img.cpu().numpy() if img is not None else pt.read_rgba32f()
+    rows_local = pt.rows_local
+    pt.close()
+    ms_per_step = dt / steps * 1e3
+    return {
+        "cfg": cfg, "scene": scene, "W": W, "H": H, "spp": spp, "bounces": bounces, "chunk": chunk,
+        "use_graph": use_graph, "value": seg_all * steps / dt / 1e6, "ms_per_step": ms_per_step,
+        "ms_per_frame": ms_per_step / spp, "cold_ms": cold_ms, "segments": seg_all, "roofline": roofline,
+        "sb": sb, "frame": frame, "rows_local": rows_local,
+    }
 
 
 def main():
@@ -114,204 +356,64 @@ def main():
     ap.add_argument("--cpu-threads", type=int, default=0, help="0 = every CPU this process may use")
     ap.add_argument("--no-cold", action="store_true", help="skip the cold first-render measurement")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--secondary", default=None,
+                    help="comma list of configs timed after the headline (default: C3,C4 for a one-GPU C2 "
+                         "run, none otherwise; 'none' to skip)")
+    ap.add_argument("--secondary-steps", type=int, default=2)
+    ap.add_argument("--share-of", type=int, default=0,
+                    help="one process renders rank 0's share of an N-way row split (its frames per launch "
+                         "too) with no collective: the per-GPU share proxy of an N-GPU run (not a scaling "
+                         "measurement)")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="nccl = RCCL over xGMI (default); gloo = CPU rehearsal of the N>1 path")
     ap.add_argument("--dump-frame", default=None,
                     help="rank 0 saves the last step's assembled RGBA32F frame here (np.save; tests)")
-    ap.add_argument("--traffic-json", default=os.path.join(REPO, "profiles", "traffic_latest.json"),
-                    help="PMC-derived HBM bytes per launch (tools/pmc_traffic.py)")
+    ap.add_argument("--traffic-json", default=None,
+                    help="PMC summary for the headline config (default profiles/pmc/<config>[_wN].json, "
+                         "tools/pmc_traffic.py)")
     args = ap.parse_args()
 
     import torch
 
-    import pt_host
-    import pt_scenes
-
-    scene, W, H, spp, bounces, chunk, graph_launches = CONFIGS[args.config]
-    W = args.width or W
-    H = args.height or H
-    spp = args.spp or spp
-    bounces = args.bounces if args.bounces is not None else bounces
     world = int(os.environ.get("WORLD_SIZE", "1"))
-    # frames per launch: the per-GPU share of the image shrinks with N, so launches get
-    # N times more frames, capped at spp (one launch tail per launch; measured: C2 on one
-    # GPU runs 2.5% faster as one 1024-frame launch than as 8 of 128, and a 1080p/8 share
-    # runs at the single-GPU rate with 1024-frame launches, 13% slower with 128).  The graph
-    # config (C5) keeps its captured launch shape.
-    if args.chunk:
-        chunk = args.chunk
-    elif graph_launches == 0:
-        chunk = chunk * world
-    chunk = min(chunk, spp)
-
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     distributed = world > 1
     ndev = max(1, torch.cuda.device_count())
     device = local_rank % ndev
+    if args.share_of > 1:
+        if distributed:
+            raise SystemExit("--share-of is a one-process proxy; do not combine it with torch.distributed.run")
+        world = args.share_of
+    ctx = dict(world=world, rank=rank, device=device, distributed=distributed)
     if distributed:
         import torch.distributed as dist
-        import pt_dist
         if args.dist_backend == "nccl":
             torch.cuda.set_device(device)
             dist.init_process_group("nccl", device_id=torch.device("cuda", device))
         else:
             dist.init_process_group("gloo")
+        ctx["dist"] = dist
 
-    def barrier():
-        if distributed:
-            dist.barrier()
+    m = measure(args.config, args, ctx, args.steps, args.warmup, cold=not args.no_cold, W=args.width,
+                H=args.height, spp=args.spp, bounces=args.bounces, chunk=args.chunk, dump=bool(args.dump_frame))
+    W, H, spp, bounces, scene = m["W"], m["H"], m["spp"], m["bounces"], m["scene"]
 
-    # the scene is generated, parsed and its BVH built once, on rank 0, then broadcast
-    # (pt_dist.broadcast_scene; RCCL for nccl) -- every rank renders the same arrays
-    scene_dir = os.path.join(REPO, "scenes")
-    sb = None
-    if rank == 0:
-        sb = pt_host.setupBuffers(*pt_scenes.write_scene(scene, scene_dir))
-    if distributed:
-        sb = pt_dist.broadcast_scene(sb, device="cuda" if args.dist_backend == "nccl" else "cpu")
-    cold_ms = None
-    if not args.no_cold and graph_launches == 0:
-        # cold first render: a fresh context right after pt_upload_scene (raster tile order
-        # until the probe launch's costs are sorted), after a tiny render on a throw-away
-        # context has loaded the code object -- what one render of a new scene costs
-        warm = pt_host.PathTracer(64, 32, max_bounce=bounces, device=device)
-        warm.upload(sb)
-        warm.render(1, 2, 0)
-        warm.close()
-        cold = pt_host.PathTracer(W, H, max_bounce=bounces, display_mode=1, device=device, rank=rank, world=world)
-        cold.set_kernel(args.variant)
-        cold.upload(sb)
-        barrier()
-        tc = time.perf_counter()
-        for f0 in range(1, spp + 1, chunk):
-            cold.render_async(f0, min(chunk, spp - (f0 - 1)), 0 if f0 == 1 else 1)
-        cold.sync()
-        cold_ms = (time.perf_counter() - tc) * 1e3
-        cold.close()
-        if distributed:
-            t = torch.tensor([cold_ms], dtype=torch.float64,
-                             device="cuda" if args.dist_backend == "nccl" else "cpu")
-            dist.all_reduce(t, op=dist.ReduceOp.MAX)
-            cold_ms = float(t.item())
-    pt = pt_host.PathTracer(W, H, max_bounce=bounces, display_mode=1, device=device, rank=rank, world=world)
-    pt.set_kernel(args.variant)
-    pt.upload(sb)
-    launches = [(f0, min(chunk, spp - (f0 - 1))) for f0 in range(1, spp + 1, chunk)]
-    use_graph = graph_launches > 0 and spp % (chunk * graph_launches) == 0
-    if use_graph:
-        pt.progressive_setup(chunk, graph_launches)
-        replays = spp // (chunk * graph_launches)
-
-    if distributed:
-        rmax = pt_dist.rows_max(H, world)
-        dev = "cuda" if args.dist_backend == "nccl" else "cpu"
-        send = torch.zeros((rmax, W, 4), dtype=torch.float32, device=dev)
-        # the rows leave the render context by a device copy in both modes (the RCCL path's
-        # pt_copy_rows_device); the gloo rehearsal then stages them through host memory
-        dsend = send if dev == "cuda" else torch.zeros((rmax, W, 4), dtype=torch.float32, device="cuda")
-
-    def step():
-        if use_graph:
-            pt.progressive_reset(1)
-            pt.progressive_run(replays, sync=False)
-        else:
-            for f0, n in launches:
-                pt.render_async(f0, n, 0 if f0 == 1 else 1)
-        pt.sync()
-        if distributed:
-            pt.copy_rows_device(dsend.data_ptr(), pt.rows_local * W * 16)
-            if args.dist_backend != "nccl":
-                send.copy_(dsend)
-            img = pt_dist.gather_image(send, H, world)
-            if args.dist_backend == "nccl":
-                torch.cuda.synchronize()
-            return img
-        return None
-
-    for _ in range(args.warmup):
-        step()
-    pt.timing(reset=True)
-    barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        img = step()
-    torch.cuda.synchronize()
-    barrier()
-    dt = time.perf_counter() - t0
-    kern_ms, n_launch = pt.timing(reset=True)
-    if use_graph:
-        n_launch = args.steps * replays * graph_launches      # events bracket whole replays
-    coll_dev = "cuda" if args.dist_backend == "nccl" else "cpu"
-    if distributed:
-        t = torch.tensor([dt], dtype=torch.float64, device=coll_dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        dt = float(t.item())
-
-    # untimed counting pass over the same frames: exact reference-semantics work counts
-    pt.set_counting(True)
-    tot = dict(segments=0, node_visits=0, tri_tests=0, sphere_tests=0, hits=0)
-    alg_bytes = 0
-    for f0, n in launches:
-        pt.render(f0, n, 0 if f0 == 1 else 1)
-        _, cnt = pt.stats()
-        for k in tot:
-            tot[k] += cnt[k]
-        alg_bytes += algorithmic_bytes(cnt, pt.rows_local * W, f0 == 1)
-    pt.set_counting(False)
-    if distributed:
-        v = torch.tensor([tot["segments"], alg_bytes], dtype=torch.float64, device=coll_dev)
-        dist.all_reduce(v, op=dist.ReduceOp.SUM)
-        seg_all = float(v[0])
-    else:
-        seg_all = float(tot["segments"])
-
-    ms_per_step = dt / args.steps * 1e3
-    value = seg_all * args.steps / dt / 1e6
-    avg_launch_ms = kern_ms / max(n_launch, 1)
-    bytes_per_launch = alg_bytes / len(launches)       # this rank's launches
-    achieved = bytes_per_launch / (avg_launch_ms * 1e-3) / 1e9
-
-    # Roofline.  The scene is LDS/L2-resident, so HBM does not bound the kernel (the algorithmic
-    # bytes exceed the HBM peak); the bound that binds is VALU issue.  Its per-launch
-    # instruction count and held clock come from a PMC pass of the same build and workload
-    # (tools/gpu_pmc.sh -> tools/pmc_traffic.py -> profiles/traffic_latest.json):
-    #   achieved = SQ_INSTS_VALU per launch / the live launch time (HIP events, this run)
-    #   peak     = 1024 SIMDs x held clock / 2 cycles per wave64 VALU instruction
-    #   busy_frac_pmc = SQ_INSTS_VALU x 2 / (1024 x GRBM_GUI_ACTIVE / 8), all from the PMC pass
-    pmc, stale, lib_sha = pmc_for(args.traffic_json, pt_host.LIB_PATH, W, H, chunk, scene, world)
-    hbm = {"algorithmic_gbs": round(achieved, 1), "algorithmic_frac": round(achieved / HBM_PEAK_GBS, 4),
-           "algorithmic_bytes_per_launch": int(bytes_per_launch), "peak": HBM_PEAK_GBS, "unit": "GB/s"}
-    roofline = {"bound": "valu", "achieved": None, "peak": None, "unit": "G wave-VALU instr/s", "frac": None,
-                "traffic": None, "avg_launch_ms": round(avg_launch_ms, 3), "n_launches": n_launch,
-                "lib_sha256": lib_sha[:16]}
-    if stale:
-        roofline["pmc_stale"] = stale
-    if pmc is not None and pmc.get("valu_instr_per_launch"):
-        cnt = pmc["counters_per_launch"]
-        vi = pmc["valu_instr_per_launch"]
-        clk = pmc["clock_ghz"]
-        roofline.update(achieved=round(vi / (avg_launch_ms * 1e-3) / 1e9, 2), peak=round(N_SIMD * clk / 2.0, 2))
-        roofline["frac"] = round(roofline["achieved"] / roofline["peak"], 4)
-        roofline["busy_frac_pmc"] = round(pmc["valu_busy_frac"], 4)
-        roofline["clock_ghz_pmc"] = round(clk, 3)
-        roofline["valu_instr_per_launch"] = vi
-        roofline["valu_instr_per_segment"] = round(vi / (seg_all / len(launches)), 2)
-        roofline["active_lanes_per_valu"] = round(pmc.get("valu_active_lanes_per_instr", 0.0), 2)
-        if pmc.get("hbm_bytes_per_launch"):
-            tb = pmc["hbm_bytes_per_launch"]
-            roofline["traffic"] = int(tb)
-            hbm.update(traffic_bytes_per_launch=int(tb), measured_gbs=round(tb / (avg_launch_ms * 1e-3) / 1e9, 1),
-                       measured_frac=round(tb / (avg_launch_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
-                       traffic_over_algorithmic=round(tb / bytes_per_launch, 2))
-        roofline["source"] = pmc.get("source", "profiles/traffic_latest.json")
-        if pmc.get("pmc_launch_ms"):   # the PMC pass's own launch time beside the live one
-            roofline["pmc_launch_ms"] = round(pmc["pmc_launch_ms"], 3)
-    roofline["hbm"] = hbm
-    roofline["basis"] = ("VALU issue: achieved = PMC SQ_INSTS_VALU per launch / live avg launch time (HIP events on "
-                         "the render stream); peak = 1024 SIMDs x PMC-held clock / 2; HBM kept as a secondary "
-                         "field (algorithmic bytes, SURVEY.md §8(d), and PMC-measured traffic)")
+    sec_cfgs = []
+    if args.secondary is None:
+        if args.config == "C2" and world == 1 and not any((args.width, args.height, args.spp, args.chunk)):
+            sec_cfgs = ["C3", "C4"]
+    elif args.secondary != "none":
+        sec_cfgs = [c for c in args.secondary.split(",") if c]
+    secondary = []
+    for c in sec_cfgs:
+        s = measure(c, args, ctx, args.secondary_steps, 1, cold=False)
+        secondary.append({
+            "config": c, "workload": "%s: %s %dx%d, %d spp in launches of %d frames, %d bounces" % (
+                c, s["scene"], s["W"], s["H"], s["spp"], s["chunk"], s["bounces"]),
+            "value": round(s["value"], 3), "unit": "Mrays/s", "steps": args.secondary_steps, "warmup": 1,
+            "ms_per_step": round(s["ms_per_step"], 3), "ms_per_frame": round(s["ms_per_frame"], 4),
+            "segments_per_step": int(s["segments"]), "roofline": s["roofline"]})
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -321,7 +423,7 @@ def main():
         if args.cpu_threads:
             threads = args.cpu_threads
         t1 = time.perf_counter()
-        _, ccnt = oracle_lib.render(sb, W, H, max_bounce=bounces, n_frames=args.cpu_spp, threads=threads,
+        _, ccnt = oracle_lib.render(m["sb"], W, H, max_bounce=bounces, n_frames=args.cpu_spp, threads=threads,
                                     counters=True)
         cdt = time.perf_counter() - t1
         cpu = {"value": round(float(ccnt[0]) / cdt / 1e6, 3), "unit": "Mrays/s", "cores": threads, "kind": "port",
@@ -333,31 +435,39 @@ def main():
 
     if args.dump_frame and rank == 0:
         import numpy as np
-        np.save(args.dump_frame, img.cpu().numpy() if img is not None else pt.read_rgba32f())
+        np.save(args.dump_frame, m["frame"])
     if rank == 0:
         line = {
-            "metric": METRIC, "value": round(value, 3), "unit": "Mrays/s", "n_gpus": world,
-            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_per_step, 3),
+            "metric": METRIC, "value": round(m["value"], 3), "unit": "Mrays/s", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(m["ms_per_step"], 3),
             "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "f32",
             "data": "synthetic",
             "config": {"workload": "%s: %s %dx%d, %d spp (frames 1..%d), %d bounces (i<=%d), AA+sky+sphere on%s"
                        % (args.config, scene, W, H, spp, spp, bounces, bounces,
-                          ", hipGraph sample loop" if use_graph else ""),
+                          ", hipGraph sample loop" if m["use_graph"] else ""),
                        "scene": scene, "width": W, "height": H, "spp": spp, "max_bounce": bounces,
-                       "frames_per_launch": chunk, "kernel_variant": args.variant,
+                       "frames_per_launch": m["chunk"], "kernel_variant": args.variant,
                        "parallelism": ("row-interleaved image split x%d + %s all-gather"
                                        % (world, "RCCL" if args.dist_backend == "nccl" else "gloo"))
                        if world > 1 else "single GPU"},
-            "ms_per_frame": round(ms_per_step / spp, 4),
-            "cold_ms_per_step": None if cold_ms is None else round(cold_ms, 3),
-            "segments_per_step": int(seg_all),
-            "roofline": roofline,
+            "ms_per_frame": round(m["ms_per_frame"], 4),
+            "cold_ms_per_step": None if m["cold_ms"] is None else round(m["cold_ms"], 3),
+            "segments_per_step": int(m["segments"]),
+            "roofline": m["roofline"],
             "cpu_baseline": cpu,
+            "secondary": secondary,
         }
+        if world > 1:
+            line["roofline"]["share"] = "rank 0's share: rows y = 0 mod %d, %d rows" % (world, m["rows_local"])
+        if args.share_of > 1:   # a proxy line: this GPU's rate on rank 0's share, n_gpus stays 1
+            line["n_gpus"] = 1
+            line["share_proxy"] = {"of": world, "rows": m["rows_local"], "note": (
+                "one GPU rendering rank 0's share of a %d-way row split (frames per launch x%d); value is this "
+                "GPU's rate, not an N-GPU measurement" % (world, world))}
+            line["config"]["parallelism"] = "share proxy: rank 0 of %d, no collective" % world
         print(json.dumps(line), flush=True)
-    pt.close()
     if distributed:
-        dist.destroy_process_group()
+        ctx["dist"].destroy_process_group()
 
 
 if __name__ == "__main__":

@@ -60,8 +60,8 @@ int pt_group_gather_rgba8_aces(pt_group* g, unsigned char* dst, size_t bytes, in
  * gather and the ACES epilogue of the frame as every context's stream has it now, then a copy
  * into pinned host buffer `buf` (0..3) behind it on the root's group stream, and returns at
  * once; renders queued afterwards wait only for the row packing.  end waits for that copy and returns the
- * pinned pixels (valid until the buffer is begun again).  The gather time (pt_group_stats)
- * is that of the last gather begun. */
+ * pinned pixels (valid until the buffer is begun again); pt_group_stats then reports that
+ * buffer's gather time. */
 int pt_group_present_begin(pt_group* g, int buf);
 int pt_group_present_end(pt_group* g, int buf, const unsigned char** pixels);
 
@@ -71,6 +71,24 @@ int pt_group_stats(const pt_group* g, double* gather_ms, size_t* bytes_per_devic
 
 /* One-shot form: create a group, gather, destroy (sets up a communicator on every call). */
 int pt_gather_rgba32f(pt_ctx* const* ctxs, int n, float* dst, size_t bytes, int dst_on_device);
+
+/* The gather plan pt_group_create computes -- host arithmetic only, no device is touched, so
+ * the multi-device layouts can be checked on any machine.  Contexts i = 0..n-1 live on
+ * device[i] with image rank rank[i] (world n, ranks 0..n-1 each once).  Out (n ints each):
+ * the distinct devices in first-use order (devices_out[0] = device[0], the root of the
+ * collectives) and their count, each context's device index and slot on that device, the
+ * slots per device (every device sends max_slots padded row blocks of ceil(H/n) rows), and
+ * table[rank] = dev_idx * max_slots + slot, the rank's block in the gathered buffer.
+ * Returns 0 or PT_E_ARG. */
+int pt_group_plan(const int* device, const int* rank, int n, int* devices_out, int* n_devices, int* dev_idx,
+                  int* slot, int* max_slots, int* table);
+
+/* The root's interleave on the host: frame (height x width RGBA32F) from n_blocks gathered
+ * blocks of ceil(height/world) x width RGBA32F by the plan's table -- the index function of
+ * the device kernel (csrc/pt_group_plan.h).  Returns 0 or PT_E_ARG (a table entry outside
+ * the blocks). */
+int pt_group_interleave_host(const float* blocks, size_t n_blocks, const int* table, int world, int width,
+                             int height, float* frame);
 
 #ifdef __cplusplus
 }

@@ -15,6 +15,7 @@
 // sits between the last render and the gather.
 #include "../../include/pt_api.h"
 #include "../../include/pt_group.h"
+#include "pt_group_plan.h"
 
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
@@ -37,15 +38,14 @@ constexpr int kGroupPresentBufs = 4;   // pt_group_present_begin buffers
 namespace {
 
 // Full frame from the gathered blocks: row y comes from image rank r = y mod G, local row
-// y div G, stored in block table[r] of rows_max rows.  One float4 per thread, coalesced.
+// y div G, stored in block table[r] of rows_max rows (ptg::interleave_src, the function
+// pt_group_interleave_host runs on the CPU).  One float4 per thread, coalesced.
 __global__ __launch_bounds__(256) void k_interleave_rows(const float4* __restrict__ blocks, const int* __restrict__ table,
                                                          float4* __restrict__ out, int W, int world, int rows_max) {
     const int x = blockIdx.x * 256 + threadIdx.x;
     const int y = blockIdx.y;
     if (x >= W) return;
-    const int r = y % world, k = y / world;
-    const size_t src = ((size_t)table[r] * (size_t)rows_max + (size_t)k) * (size_t)W + (size_t)x;
-    out[(size_t)y * (size_t)W + (size_t)x] = blocks[src];
+    out[(size_t)y * (size_t)W + (size_t)x] = blocks[ptg::interleave_src(x, y, W, world, rows_max, table)];
 }
 
 }  // namespace
@@ -70,6 +70,7 @@ struct pt_group {
     uchar4* present_dev[kGroupPresentBufs] = {};
     unsigned char* present_host[kGroupPresentBufs] = {};
     hipEvent_t ev_copied[kGroupPresentBufs] = {};
+    hipEvent_t ev_g0[kGroupPresentBufs] = {}, ev_g1[kGroupPresentBufs] = {};   // its gather's timer
     bool present_pending[kGroupPresentBufs] = {};
     uchar4* rgba8 = nullptr;                // root: the ACES frame of pt_group_gather_rgba8_aces
     double last_ms = 0.0;
@@ -120,6 +121,8 @@ void pt_group_destroy(pt_group* g) {
             (void)hipFree(g->present_dev[b]);
             if (g->present_host[b]) (void)hipHostFree(g->present_host[b]);
             if (g->ev_copied[b]) (void)hipEventDestroy(g->ev_copied[b]);
+            if (g->ev_g0[b]) (void)hipEventDestroy(g->ev_g0[b]);
+            if (g->ev_g1[b]) (void)hipEventDestroy(g->ev_g1[b]);
         }
         (void)hipFree(g->rgba8);
         (void)hipFree(g->recv);
@@ -160,24 +163,22 @@ int pt_group_create(pt_ctx* const* ctxs, int n, pt_group** out) {
         if (cfg[i].rank < 0 || cfg[i].rank >= n || seen[cfg[i].rank]++)
             return gfail(g, PT_E_ARG, "context ranks must be 0..world-1, each once");
     }
-    g->rows_max = (g->H + g->world - 1) / g->world;
+    g->rows_max = ptg::rows_max(g->H, g->world);
+    // devices, slots and the block table: pt_group_plan (host arithmetic, CPU-tested)
+    std::vector<int> dev_of(n), rank_of(n), devs(n), table(n);
+    for (int i = 0; i < n; i++) {
+        dev_of[i] = cfg[i].device;
+        rank_of[i] = cfg[i].rank;
+    }
     g->dev_idx.assign(n, 0);
     g->slot.assign(n, 0);
+    int n_dev = 0;
+    if (pt_group_plan(dev_of.data(), rank_of.data(), n, devs.data(), &n_dev, g->dev_idx.data(), g->slot.data(),
+                      &g->max_slots, table.data()))
+        return gfail(g, PT_E_ARG, "group plan");
+    g->devs.assign(devs.begin(), devs.begin() + n_dev);
     g->rows_local.assign(n, 0);
-    std::vector<int> used;
-    for (int i = 0; i < n; i++) {
-        auto it = std::find(g->devs.begin(), g->devs.end(), cfg[i].device);
-        if (it == g->devs.end()) {
-            g->devs.push_back(cfg[i].device);
-            used.push_back(0);
-            it = g->devs.end() - 1;
-        }
-        const int d = (int)(it - g->devs.begin());
-        g->dev_idx[i] = d;
-        g->slot[i] = used[d]++;
-        pt_rows(ctxs[i], &g->rows_local[i], nullptr, nullptr);
-    }
-    g->max_slots = *std::max_element(used.begin(), used.end());
+    for (int i = 0; i < n; i++) pt_rows(ctxs[i], &g->rows_local[i], nullptr, nullptr);
     const int nd = (int)g->devs.size();
     g->comm.assign(nd, nullptr);
     GNCCL(g, ncclCommInitAll(g->comm.data(), nd, g->devs.data()));
@@ -199,8 +200,6 @@ int pt_group_create(pt_ctx* const* ctxs, int n, pt_group** out) {
     GHIP(g, hipSetDevice(g->devs[0]));
     GHIP(g, hipMalloc(&g->recv, std::max<size_t>(blk * (size_t)g->max_slots * (size_t)nd, 16)));
     GHIP(g, hipMalloc(&g->frame, std::max<size_t>((size_t)g->W * (size_t)g->H * sizeof(float4), 16)));
-    std::vector<int> table(g->world);
-    for (int i = 0; i < n; i++) table[cfg[i].rank] = g->dev_idx[i] * g->max_slots + g->slot[i];
     GHIP(g, hipMalloc(&g->d_table, table.size() * sizeof(int)));
     GHIP(g, hipMemcpy(g->d_table, table.data(), table.size() * sizeof(int), hipMemcpyHostToDevice));
     GHIP(g, hipEventCreate(&g->ev0));
@@ -264,7 +263,7 @@ int pt_group_upload_scene(pt_group* g, const float* tris, int n_tris, const floa
 // k_interleave_rows writes the frame to `out` (root device memory).  Each context's stream
 // then waits for its device's pack, so renders queued after this call cannot overwrite rows
 // that are still being packed.  Nothing is synchronised here.
-static int gather_core(pt_group* g, float4* out) {
+static int gather_core(pt_group* g, float4* out, hipEvent_t e0, hipEvent_t e1) {
     const int n = (int)g->ctx.size(), nd = (int)g->devs.size();
     const size_t blk = block_floats(g);
     // the device streams wait for every context's pending renders first; the timer starts
@@ -283,7 +282,7 @@ static int gather_core(pt_group* g, float4* out) {
         GHIP(g, hipStreamWaitEvent(g->stream[0], g->ctx_ev[i], 0));
     }
     GHIP(g, hipSetDevice(g->devs[0]));
-    GHIP(g, hipEventRecord(g->ev0, g->stream[0]));
+    GHIP(g, hipEventRecord(e0, g->stream[0]));
     // pack: each context's rows into its block
     for (int i = 0; i < n; i++) {
         const int d = g->dev_idx[i];
@@ -318,7 +317,7 @@ static int gather_core(pt_group* g, float4* out) {
                            g->stream[0], g->recv, g->d_table, out, g->W, g->world, g->rows_max);
         GHIP(g, hipGetLastError());
     }
-    GHIP(g, hipEventRecord(g->ev1, g->stream[0]));
+    GHIP(g, hipEventRecord(e1, g->stream[0]));
     return PT_OK;
 }
 
@@ -341,7 +340,7 @@ int pt_group_gather_rgba32f(pt_group* g, float* dst, size_t bytes, int dst_on_de
     const size_t frame_bytes = (size_t)g->W * (size_t)g->H * sizeof(float4);
     if (bytes < frame_bytes) return gfail(g, PT_E_ARG, "destination too small");
     float4* out = dst_on_device ? (float4*)dst : g->frame;
-    int rc = gather_core(g, out);
+    int rc = gather_core(g, out, g->ev0, g->ev1);
     if (rc) return rc;
     if (!dst_on_device) GHIP(g, hipMemcpyAsync(dst, g->frame, frame_bytes, hipMemcpyDeviceToHost, g->stream[0]));
     return gather_finish(g);
@@ -353,7 +352,7 @@ int pt_group_gather_rgba8_aces(pt_group* g, unsigned char* dst, size_t bytes, in
     if (bytes < (size_t)n * 4) return gfail(g, PT_E_ARG, "destination too small");
     GHIP(g, hipSetDevice(g->devs[0]));
     if (!g->rgba8 && !dst_on_device) GHIP(g, hipMalloc(&g->rgba8, std::max<long long>(n, 1) * sizeof(uchar4)));
-    int rc = gather_core(g, g->frame);
+    int rc = gather_core(g, g->frame, g->ev0, g->ev1);
     if (rc) return rc;
     void* out = dst_on_device ? (void*)dst : (void*)g->rgba8;
     rc = pt__aces_launch(g->frame, out, n, g->stream[0]);
@@ -372,11 +371,13 @@ int pt_group_present_begin(pt_group* g, int buf) {
         GHIP(g, hipHostMalloc((void**)&g->present_host[buf], std::max<long long>(n, 1) * sizeof(uchar4),
                               hipHostMallocDefault));
         GHIP(g, hipEventCreateWithFlags(&g->ev_copied[buf], hipEventDisableTiming));
+        GHIP(g, hipEventCreate(&g->ev_g0[buf]));
+        GHIP(g, hipEventCreate(&g->ev_g1[buf]));
     }
     // a buffer begun again before its end: its previous copy must land first
     if (g->present_pending[buf]) GHIP(g, hipEventSynchronize(g->ev_copied[buf]));
     g->present_pending[buf] = false;
-    int rc = gather_core(g, g->frame);
+    int rc = gather_core(g, g->frame, g->ev_g0[buf], g->ev_g1[buf]);
     if (rc) return rc;
     GHIP(g, hipSetDevice(g->devs[0]));
     rc = pt__aces_launch(g->frame, g->present_dev[buf], n, g->stream[0]);
@@ -398,6 +399,10 @@ int pt_group_present_end(pt_group* g, int buf, const unsigned char** pixels) {
     GHIP(g, hipSetDevice(g->devs[0]));
     GHIP(g, hipEventSynchronize(g->ev_copied[buf]));
     g->present_pending[buf] = false;
+    // this buffer's own gather timer (a later begin re-records only its own buffer's events)
+    float ms = 0.0f;
+    GHIP(g, hipEventElapsedTime(&ms, g->ev_g0[buf], g->ev_g1[buf]));
+    g->last_ms = ms;
     *pixels = g->present_host[buf];
     return PT_OK;
 }

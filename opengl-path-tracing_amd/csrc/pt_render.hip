@@ -96,6 +96,7 @@ struct KParams {
     float cons_m[3];               // ... 2^-19 * the scene's largest |coordinate| per axis, rounded up
     int wide_top;                  // wide walk (WIDE instantiations): records [0, wide_top) staged in LDS
     float wide_cw[3];              // ... 2^-18 * the scene's largest |coordinate| per axis, rounded up (WRay)
+    int leaf_cert;                 // culling / wide walk: skip the exact leaf re-test where the hit certifies it
 };
 
 // Progressive mode (hipGraph replay): the frame range comes from a device counter, and
@@ -398,13 +399,17 @@ __device__ __forceinline__ float tri_plane(float4 nd, f3 o, f3 d) {    // nd: qu
 }
 // The three edge tests (:299-306) of triangle `slot` at p with normal n: the caller has n
 // from the plane test (quad 0), so only the vertices (quads 1-3) are read.
+// With `cert_on` (wave-uniform) it also evaluates the leaf re-test certificate of this
+// triangle at p (ptw::leaf_certificate, pt_wide.h): its vertices are at hand here.
 template <bool LDS>
-__device__ __forceinline__ bool tri_edges_at(const SceneView& S, int slot, f3 n, f3 p) {
+__device__ __forceinline__ bool tri_edges_at(const SceneView& S, int slot, f3 n, f3 p, bool cert_on, float omax,
+                                             bool& cert) {
     const float4 q1 = tri_quad<LDS>(S, slot, 1), q2 = tri_quad<LDS>(S, slot, 2), q3 = tri_quad<LDS>(S, slot, 3);
     const f3 v0 = mk(q1.x, q1.y, q1.z), v1 = mk(q2.x, q2.y, q2.z), v2 = mk(q3.x, q3.y, q3.z);
     const float e0 = pt::dot(n, pt::cross(v1 - v0, p - v0));
     const float e1 = pt::dot(n, pt::cross(v2 - v1, p - v1));
     const float e2 = pt::dot(n, pt::cross(v0 - v2, p - v2));
+    if (cert_on) cert = ptw::leaf_certificate(p, n, v0, v1, v2, omax);
     return (e0 > 0.0f) & (e1 > 0.0f) & (e2 > 0.0f);
 }
 // The lane's index in its wave, recomputed where it is used (two VALU): a value held across
@@ -437,9 +442,12 @@ __device__ __forceinline__ float fperm_f(int dst_bytes, float v) {
 // test runs the same operations on the same values as at its source lane: the same bits.
 // Returns (through h1 / h2) the hit_triangle results up to that equivalence.
 // nda: quad 0 {n, d0} of slot s0; cop: the leaf code's coplanar bit.
+// cert_on (wave-uniform): also return each triangle's leaf re-test certificate (ca / cb, for
+// a triangle whose edge tests pass; omax = max_i |o_i|), computed by the lane that tests it.
 template <bool LDS>
 __device__ __forceinline__ void leaf_pair_tests(const SceneView& S, bool at, int s0, float4 nda, bool cop,
-                                                f3 o, f3 d, float t, int max_pairs, float& h1, float& h2) {
+                                                f3 o, f3 d, float t, int max_pairs, float& h1, float& h2,
+                                                bool cert_on, bool& cta, bool& ctb) {
     float ta = 0.0f, tb = 0.0f;
     if (at) ta = tri_plane<LDS>(nda, o, d);
     // a coplanar pair (n and d0 equal up to the sign of zero components, flagged at upload)
@@ -460,6 +468,7 @@ __device__ __forceinline__ void leaf_pair_tests(const SceneView& S, bool at, int
     const unsigned long long ma = __ballot(na), mb = __ballot(nb);
     const int ca = __popcll(ma), n = ca + __popcll(mb);
     bool oka = false, okb = false;
+    const float omax = ptw::abs_max3(o);
     if (n <= max_pairs) {      // max_pairs <= 63 (tuning key 7; 0 = every lane tests its own)
         const int lane = lane_id();
         const int ja = rank_in(ma), jb = ca + rank_in(mb);
@@ -486,14 +495,26 @@ __device__ __forceinline__ void leaf_pair_tests(const SceneView& S, bool at, int
             const float nbx = fperm_f(db, nb3.x), nby = fperm_f(db, nb3.y), nbz = fperm_f(db, nb3.z);
             wn = first ? mk(nax, nay, naz) : mk(nbx, nby, nbz);
         }
-        bool pass = false;
-        if (lane < n) pass = tri_edges_at<LDS>(S, ws, wn, wp);
+        bool pass = false, cert = false;
+        float wom = 0.0f;
+        if (cert_on) {
+            const float oa = fperm_f(da, omax), ob = fperm_f(db, omax);
+            wom = first ? oa : ob;
+        }
+        if (lane < n) pass = tri_edges_at<LDS>(S, ws, wn, wp, cert_on, wom, cert);
         const unsigned long long r = __ballot(pass);
         oka = na & (((r >> ja) & 1ull) != 0ull);
         okb = nb & (((r >> jb) & 1ull) != 0ull);
+        if (cert_on) {
+            const unsigned long long rc = __ballot(pass & cert);
+            cta = oka & (((rc >> ja) & 1ull) != 0ull);
+            ctb = okb & (((rc >> jb) & 1ull) != 0ull);
+        }
     } else {
-        if (na) oka = tri_edges_at<LDS>(S, s0, na3, o + d * ta);
-        if (nb) okb = tri_edges_at<LDS>(S, s0 + 1, nb3, o + d * tb);
+        if (na) oka = tri_edges_at<LDS>(S, s0, na3, o + d * ta, cert_on, omax, cta);
+        if (nb) okb = tri_edges_at<LDS>(S, s0 + 1, nb3, o + d * tb, cert_on, omax, ctb);
+        cta = cta & oka;
+        ctb = ctb & okb;
     }
     h1 = oka ? ta : -1.0f;
     h2 = okb ? tb : -1.0f;
@@ -716,7 +737,15 @@ __device__ __forceinline__ void trav_wide(const SceneView& S, f3 o, f3 rd, float
     for (;;) {
 #pragma unroll
         for (int u = 0; u < PT_WIDE_UNROLL; u++) {
-            const bool on = cur >= 0;
+            bool on = cur >= 0;
+#ifdef PT_WIDE_DEEP_MIN
+            {   // experiment: lanes at global records wait while fewer than PT_WIDE_DEEP_MIN of
+                // them are due and some lane still walks LDS records
+                const bool deep = on & ((cur >> 3) >= S.wtop);
+                const int nd = __popcll(__ballot(deep));
+                if (nd < PT_WIDE_DEEP_MIN && __ballot(on & !deep)) on = on & !deep;
+            }
+#endif
             float4 q0, q1, q2;
             wrec_at(S, on ? cur >> 3 : 0, q0, q1, q2);
             const uint32_t pend = ptw::wide_hits(q0.x, q0.y, q0.z, __float_as_uint(q0.w), __float_as_uint(q1.x),
@@ -1144,6 +1173,7 @@ __global__ __launch_bounds__(NT, MINW) void k_render_sm(KParams p) {
                 if (LDS && (fast & (cont >= 0))) cont += oct_base(d, S.np << 5);
             }
             float h1 = -1.0f, h2 = -1.0f;
+            bool ca = false, cb = false;   // the chosen triangle certifies its leaf's box (pt_wide.h)
             if (p.flags & PT_FLAG_MOLLER_TRUMBORE) {   // wave-uniform
                 if (at) {
                     h1 = tri_mt(tri_quad<LDS>(S, s0, 1), tri_quad<LDS>(S, s0, 2), tri_quad<LDS>(S, s0, 3), o, d);
@@ -1151,7 +1181,7 @@ __global__ __launch_bounds__(NT, MINW) void k_render_sm(KParams p) {
                                 tri_quad<LDS>(S, s0 + 1, 3), o, d);
                 }
             } else {
-                leaf_pair_tests<LDS>(S, at, s0, nd0, cop, o, d, t, p.compact_max, h1, h2);
+                leaf_pair_tests<LDS>(S, at, s0, nd0, cop, o, d, t, p.compact_max, h1, h2, p.leaf_cert != 0, ca, cb);
             }
             bool c1 = false, c2 = false;
             if (at) {
@@ -1163,7 +1193,7 @@ __global__ __launch_bounds__(NT, MINW) void k_render_sm(KParams p) {
                 // this leaf's triangles only if its box passes the exact test at this t, and
                 // only a triangle that moves t makes the difference (a leaf's hit and miss
                 // links are the same next-right).  Its image-0 offset: slot 2k+1 quad 3 .w.
-                const bool chk = at & fast & (c1 | c2);
+                const bool chk = at & fast & ((c1 & !ca) | (c2 & !cb));
                 if (__any(chk)) {
                     if (chk) {
                         float4 lo, hi;
@@ -1173,14 +1203,23 @@ __global__ __launch_bounds__(NT, MINW) void k_render_sm(KParams p) {
                     }
                 }
             }
+#ifdef PT_EXP_NO_BOXCHK
+            if (false) {   // timing experiment only (not the reference's image)
+#else
             if (WIDE) {
+#endif
                 // the wide walk reached this leaf on the conservative test: as the culling walk,
                 // its own box is tested exactly at this t before a triangle may move t (leaf g's
-                // box at wlbox[2g], [2g + 1])
-                const bool chk = at & fast & (c1 | c2);
+                // box at wlbox[2g], [2g + 1]) -- unless the chosen triangle certifies that test
+                const bool chk = at & fast & ((c1 & !ca) | (c2 & !cb));
                 if (__any(chk)) {
                     if (chk) {
+#ifdef PT_WIDE_BOX_IN_REC
+                        const float4* lb = S.wrec + kWideStride * (s0 >> 1);
+                        if (!slab_fast(lb[0], lb[1], o, d, rd, t)) c1 = c2 = false;
+#else
                         if (!slab_fast(S.wlbox[s0], S.wlbox[s0 + 1], o, d, rd, t)) c1 = c2 = false;
+#endif
                     }
                 }
             }
@@ -1441,6 +1480,8 @@ struct pt_ctx {
     int n_wide = 0;                 // wide index space (records + leaves)
     float wide_cw[3] = {0, 0, 0};
     int wide_off = 0;               // tuning key 16: 1 = the binary global walk
+    int cert_off = 0;               // tuning key 19: 1 = always run the exact leaf re-test
+    bool leaf_cert_ok = false;      // every leaf box contains its triangles' vertices (pt_wide.h certificate)
     int wide_threads = 0;           // tuning key 17: threads per block of the wide walk (0 = automatic)
     int overlap_bpc = 0;            // tuning key 18: render blocks per CU of overlapped short launches (0 = automatic)
     unsigned long long* d_counters = nullptr;
@@ -1886,6 +1927,9 @@ int pt_upload_scene(pt_ctx* c, const float* tris, int n_tris, const float* bvh, 
             const float* nd = bvh + 12 * (size_t)i;
             if (!(nd[8] > -1.0f)) continue;
             const int g = wt.g_of[i], t0 = (int)nd[8], t1 = (int)nd[9];
+            // a leaf no walk reaches (not in the nested tree from the root, which is all the
+            // links of reachable nodes lead to) has no index: nothing to place
+            if (g < 0) continue;
             const int a = ~((g << 2) | (cop_of[i] ? 2 : 0) | (t0 == t1 ? 1 : 0));
             std::memcpy(&dnw[2 * (size_t)pos[i] + 1].z, &a, 4);
             put_tri(&dtw[8 * (size_t)g], t0);
@@ -1948,6 +1992,20 @@ int pt_upload_scene(pt_ctx* c, const float* tris, int n_tris, const float* bvh, 
     }
     c->walk_nested = nested;
     c->wide_ok = wide;
+    // the leaf re-test certificate (ptw::leaf_certificate) needs each leaf box to contain its
+    // triangles' vertices -- the reference builder expands leaf boxes over them (bvh.h:29-52);
+    // an uploaded tree is checked, not assumed
+    c->leaf_cert_ok = true;
+    for (int i = 0; i < n_nodes && c->leaf_cert_ok; i++) {
+        const float* nd = bvh + 12 * (size_t)i;
+        if (!(nd[8] > -1.0f)) continue;
+        for (int k = 0; k < 2 && c->leaf_cert_ok; k++) {
+            const float* t = tris + 16 * (size_t)(int)nd[8 + k];
+            for (int v = 0; v < 3; v++)
+                for (int q = 0; q < 3; q++)
+                    if (!(nd[q] <= t[4 * v + q] && t[4 * v + q] <= nd[4 + q])) c->leaf_cert_ok = false;
+        }
+    }
     c->order_sorted = false;      // the next sort pools the new scene's first short launches
     c->order_skip = 0;
     if (n_nodes > 0) {   // every box lies in the root box (nested): M_i bounds each |coordinate|
@@ -2053,6 +2111,12 @@ int pt_set_tuning(pt_ctx* c, int key, int value) {
         if (value != 0 && value != 256 && value != 512 && value != 768 && value != 1024)
             return fail(c, PT_E_ARG, "wide walk workgroup: 256, 512, 768 or 1024 threads (0 = automatic)");
         c->wide_threads = value;
+        drop_graph(c);
+        return PT_OK;
+    }
+    if (key == 19) {
+        if (value != 0 && value != 1) return fail(c, PT_E_ARG, "leaf re-test certificate: 0 = automatic, 1 = off");
+        c->cert_off = value;
         drop_graph(c);
         return PT_OK;
     }
@@ -2316,6 +2380,8 @@ static int enqueue_render(pt_ctx* c, int frame_first, int n_frames, int acc_firs
     p.n_mats = c->n_mats;
     p.scene_fast = c->scene_fast;
     p.cons_walk = cons_walk_on(c);
+    // the certificate stands on hit_triangle's plane distance: not in Moller-Trumbore mode
+    p.leaf_cert = c->leaf_cert_ok && !c->cert_off && !(c->cfg.flags & PT_FLAG_MOLLER_TRUMBORE);
     p.sc.walk_sk = c->d_walk_sk;
     std::memcpy(p.cons_m, c->cons_m, sizeof(p.cons_m));
     std::memcpy(p.root_box, c->root_box, sizeof(p.root_box));
@@ -2454,7 +2520,11 @@ static int enqueue_render(pt_ctx* c, int frame_first, int n_frames, int acc_firs
         const size_t shade_bytes = (size_t)(3 * c->n_mats + 2 * c->n_spheres) * sizeof(float4);
         p.shade_lds = shade_bytes <= 4096;
         if (use_wide) {   // top records: 48 B each, within the block's share of the CU's LDS
-            const size_t blocks_cu = wide_nt == 1024 ? 1 : (size_t)(6 * 256 / wide_nt);
+            // (256-thread blocks: one per resident wave per SIMD, the instantiation's 5-7; the
+            // raysPerPixel > 1 one is built for 6)
+            const size_t blocks_cu = wide_nt == 1024 ? 1
+                                   : (wide_nt == 256 ? (size_t)(p.rpp > 1 ? 6 : std::min(std::max(mw, 5), 7))
+                                                     : (size_t)(6 * 256 / wide_nt));
             // (1 KiB below the even share: the allocation granule must not cost a block per CU)
             p.wide_top = (int)std::min<size_t>({(size_t)c->n_wide, (size_t)kWideTopMax,
                                                 ((size_t)160 * 1024 / blocks_cu - (p.shade_lds ? shade_bytes : 0) - 1024) / 48});
@@ -2764,6 +2834,7 @@ int pt__scene_replicate_layout(pt_ctx* dst, const pt_ctx* src, void* dptr[10], c
     dst->walk_nested = src->walk_nested;
     std::memcpy(dst->cons_m, src->cons_m, sizeof(dst->cons_m));
     dst->wide_ok = src->wide_ok;
+    dst->leaf_cert_ok = src->leaf_cert_ok;
     dst->n_wide = src->n_wide;
     std::memcpy(dst->wide_cw, src->wide_cw, sizeof(dst->wide_cw));
     dst->walk_np = src->walk_np;

@@ -11,6 +11,12 @@
 namespace ptw {
 namespace {
 
+#ifndef PT_WIDE_ORDER
+#define PT_WIDE_ORDER 0
+#endif
+constexpr int kWideOrder = PT_WIDE_ORDER;   // group numbering below the top (see wide_build)
+constexpr int kTopBreadth = 4096;           // indices numbered breadth-first first (>= any LDS top)
+
 struct BN {
     float lo[3], hi[3];
     int left = -1, right = -1;
@@ -129,35 +135,65 @@ int wide_build(const float* bvh, int n_nodes, const unsigned char* leaf_cop, Wid
         }
         return n;
     };
-    // breadth-first numbering: a record's children take consecutive indices (cbase + j)
+    // numbering: a record's children take consecutive indices (cbase + j).  Groups are
+    // allocated breadth-first until kTopBreadth indices (the records the kernel may stage in
+    // LDS come first), then -- PT_WIDE_ORDER 1 -- each remaining subtree is numbered depth-first
+    // (its groups contiguous), or -- 2 -- breadth-first inside the subtree, or -- 0 -- the
+    // breadth-first order continues over the whole tree.
     out.g_of.assign(n_nodes, -1);
-    std::vector<int> recs{0}, rdepth{0};          // binary node of each record, in g order
+    std::vector<int> recs{0}, rdepth{0};          // binary node of each record, in discovery order
     std::vector<int> parent_g{-1}, parent_slot{0};
-    std::vector<int> g_of_rec;                     // record position -> g
-    std::vector<std::array<int, 4>> kids;
-    std::vector<int> nkids;
+    std::vector<int> g_of_rec;                     // record (discovery index) -> g
+    std::vector<std::array<int, 4>> kids(1);
+    std::vector<int> nkids(1, 0);
     out.g_of[0] = 0;
     int next = 1;
     g_of_rec.push_back(0);
-    for (size_t qi = 0; qi < recs.size(); qi++) {
+    bool overflow = false;
+    // allocates record ri's child group; returns the discovery indices of its record children
+    auto process = [&](size_t ri, std::vector<int>* found) {
         int f[4];
-        const int n = frontier(recs[qi], f);
+        const int n = frontier(recs[ri], f);
         std::array<int, 4> k = {-1, -1, -1, -1};
         for (int j = 0; j < n; j++) {
             k[j] = f[j];
-            if (next >= kMaxRecords) return -1;
+            if (next >= kMaxRecords) { overflow = true; return; }
             out.g_of[f[j]] = next++;
             if (!bn[f[j]].leaf) {
+                if (found) found->push_back((int)recs.size());
                 recs.push_back(f[j]);
-                rdepth.push_back(rdepth[qi] + 1);
-                parent_g.push_back(g_of_rec[qi]);
+                rdepth.push_back(rdepth[ri] + 1);
+                parent_g.push_back(g_of_rec[ri]);
                 parent_slot.push_back(j);
                 g_of_rec.push_back(out.g_of[f[j]]);
+                kids.emplace_back();
+                nkids.push_back(0);
             }
         }
-        kids.push_back(k);
-        nkids.push_back(n);
+        kids[ri] = k;
+        nkids[ri] = n;
+    };
+    size_t qi = 0;
+    for (; qi < recs.size() && (kWideOrder == 0 || next < kTopBreadth) && !overflow; qi++) process(qi, nullptr);
+    const size_t pending = recs.size();
+    for (size_t r0 = qi; r0 < pending && !overflow; r0++) {   // the subtrees below the breadth-first top
+        std::vector<int> work{(int)r0}, found;
+        for (size_t w = 0; w < work.size() && !overflow;) {
+            int ri;
+            if (kWideOrder == 1) { ri = work.back(); work.pop_back(); }   // depth-first
+            else ri = work[w++];                                          // breadth-first in the subtree
+            found.clear();
+            process((size_t)ri, &found);
+            if (kWideOrder == 1) {
+                for (auto it = found.rbegin(); it != found.rend(); ++it) work.push_back(*it);
+                if (work.empty()) break;
+                w = 0;
+            } else {
+                work.insert(work.end(), found.begin(), found.end());
+            }
+        }
     }
+    if (overflow) return -1;
     out.n_index = next;
     out.bn_of.assign(next, -1);
     for (int i = 0; i < n_nodes; i++)
@@ -207,6 +243,9 @@ int wide_build(const float* bvh, int n_nodes, const unsigned char* leaf_cop, Wid
             float* b = &out.lbox[(size_t)out.g_of[c] * 8];
             b[0] = bn[c].lo[0]; b[1] = bn[c].hi[0]; b[2] = bn[c].lo[1]; b[3] = bn[c].hi[1];
             b[4] = bn[c].lo[2]; b[5] = bn[c].hi[2];
+            // ... and in the leaf's own (otherwise unused) record slot: the leaf phase's exact
+            // re-test reads it there, beside its siblings
+            std::memcpy(&out.rec[(size_t)out.g_of[c] * 16], b, 8 * sizeof(float));
             out.n_leaves++;
         }
     }

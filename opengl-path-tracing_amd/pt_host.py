@@ -55,6 +55,7 @@ class ViewerFrame(C.Structure):
 
 _lib = None
 _F = np.ctypeslib.ndpointer(np.float32, flags="C_CONTIGUOUS")
+_I = np.ctypeslib.ndpointer(np.int32, flags="C_CONTIGUOUS")
 
 
 def build(force=False):
@@ -127,6 +128,8 @@ def lib():
             "pt_group_present_begin": (ip, [vp, ip]),
             "pt_group_present_end": (ip, [vp, ip, C.POINTER(C.POINTER(C.c_ubyte))]),
             "pt_gather_rgba32f": (ip, [C.POINTER(vp), ip, vp, C.c_size_t, ip]),
+            "pt_group_plan": (ip, [_I, _I, ip, _I, C.POINTER(ip), _I, _I, C.POINTER(ip), _I]),
+            "pt_group_interleave_host": (ip, [_F, C.c_size_t, _I, ip, ip, ip, _F]),
             "pt_viewer_create": (ip, [vp, ip, C.POINTER(vp)]),
             "pt_viewer_destroy": (None, [vp]),
             "pt_viewer_set_params": (ip, [vp, fp, fp, ip]),
@@ -580,6 +583,32 @@ class Group:
         if getattr(self, "h", None) is not None and self.h.value:
             lib().pt_group_destroy(self.h)
         self.h = C.c_void_p()
+
+
+def group_plan(devices, ranks):
+    """pt_group_plan (host arithmetic, no device): -> dict(devices, dev_idx, slot, max_slots,
+    table) for contexts on `devices` with image `ranks`."""
+    n = len(devices)
+    dev = np.ascontiguousarray(devices, np.int32)
+    rk = np.ascontiguousarray(ranks, np.int32)
+    devs, dev_idx, slot, table = (np.zeros(n, np.int32) for _ in range(4))
+    nd, ms = C.c_int(0), C.c_int(0)
+    rc = lib().pt_group_plan(dev, rk, n, devs, C.byref(nd), dev_idx, slot, C.byref(ms), table)
+    if rc:
+        raise PTError(rc, "pt_group_plan: ranks must be 0..n-1, each once")
+    return dict(devices=devs[:nd.value].tolist(), dev_idx=dev_idx, slot=slot, max_slots=ms.value, table=table)
+
+
+def group_interleave_host(blocks, table, world, width, height):
+    """pt_group_interleave_host: the root's interleave of gathered row blocks on the host."""
+    b = np.ascontiguousarray(blocks, np.float32)
+    n_blocks = b.size // (max(1, -(-height // world)) * width * 4) if width and height else 0
+    out = np.zeros((height, width, 4), np.float32)
+    rc = lib().pt_group_interleave_host(b.reshape(-1), n_blocks, np.ascontiguousarray(table, np.int32), world,
+                                        width, height, out.reshape(-1))
+    if rc:
+        raise PTError(rc, "pt_group_interleave_host: table entry outside the blocks")
+    return out
 
 
 def gather_rgba32f(tracers, device_ptr=None):

@@ -94,3 +94,36 @@ def test_bench_roofline_needs_the_profiled_build(tmp_path):
     assert pmc is None and "another workload" in stale
     pmc, stale, _ = bench.pmc_for(str(tmp_path / "missing.json"), str(lib), 1920, 1080, 1024, "cornell", 1)
     assert pmc is None and "no PMC pass" in stale
+
+
+def test_bench_roofline_per_rank_share_and_bounds(tmp_path):
+    """At N > 1 rank 0's line may carry the roofline of its own share when the PMC pass was of
+    that share (world recorded in the summary); the bound is the unit with the larger
+    utilisation, with occupancy from SQ_WAVE_CYCLES (quad-cycles) against 8 wave slots."""
+    import hashlib
+    import json
+    import bench
+    lib = tmp_path / "libptrace.so"
+    lib.write_bytes(b"build A")
+    sha = hashlib.sha256(b"build A").hexdigest()
+    tj = tmp_path / "C2_w2.json"
+    clk, t_ms = 2.4, 100.0
+    cyc = clk * 1e9 * t_ms * 1e-3            # cycles of the launch
+    ctr = {"SQ_INSTS_VALU": 0.5 * 512 * cyc,   # VALU busy 0.5 of 1024 SIMDs x clk / 2
+           "TD_TD_BUSY_sum": 0.9 * 256 * cyc,  # TD busy 0.9
+           "SQ_WAVE_CYCLES": 6.0 * 1024 * cyc / 4.0, "GRBM_GUI_ACTIVE": 8 * cyc,
+           "SQ_THREAD_CYCLES_VALU": 40.0 * 1e9, "SQ_ACTIVE_INST_VALU": 1e9,
+           "TCC_HIT_sum": 90.0, "TCC_MISS_sum": 10.0}
+    tj.write_text(json.dumps(dict(scene="cornell", width=1920, height=1080, chunk=2048, world=2, lib_sha256=sha,
+                                  counters_per_launch=ctr, clock_ghz=clk)))
+    pmc, stale, _ = bench.pmc_for(str(tj), str(lib), 1920, 1080, 2048, "cornell", 2)
+    assert pmc is not None and stale is None
+    pmc1, stale1, _ = bench.pmc_for(str(tj), str(lib), 1920, 1080, 2048, "cornell", 1)
+    assert pmc1 is None and "another workload" in stale1
+    r = bench.roofline_from(pmc, None, sha, t_ms, 1, 1e9, 1e12)
+    assert r["bound"] == "texture" and abs(r["frac"] - 0.9) < 1e-3
+    assert abs(r["bounds"]["valu"]["frac"] - 0.5) < 1e-3
+    assert abs(r["occupancy"]["waves_per_simd"] - 6.0) < 1e-6 and r["occupancy"]["peak"] == 8
+    assert r["active_lanes_per_valu"] == 40.0 and r["memory_pipe"]["l2_hit_rate"] == 0.9
+    none = bench.roofline_from(None, "no PMC pass", sha, t_ms, 1, 1e9, 1e12)
+    assert none["frac"] is None and none["pmc_stale"] == "no PMC pass"

@@ -1,5 +1,5 @@
-"""bench.py's N>1 path with the HIP kernels: two ranks on device 0 over
-gloo run the bench's own pt_dist.broadcast_scene -> pt_copy_rows_device -> pt_dist.gather_image
+"""bench.py's N>1 path with the HIP kernels: 2, 3 and 8 ranks on device 0 over
+gloo (8 ranks on C4's 249k-triangle scene, the configuration BASELINE sends to 8 GPUs) run the bench's own pt_dist.broadcast_scene -> pt_copy_rows_device -> pt_dist.gather_image
 path; rank 0's assembled frame must equal one context's render bit for bit (each pixel's RNG
 stream depends only on (x, y, frame), computeShader.c:514-515).  RCCL cannot put two ranks on
 one GPU, so the 8-GPU RCCL run stays the driver's; tests/test_dist.py checks the gather on CPU.
@@ -28,7 +28,7 @@ def _free_port():
     return p
 
 
-@pytest.mark.parametrize("world,config", [(2, "C2"), (3, "C3")])
+@pytest.mark.parametrize("world,config", [(2, "C2"), (3, "C3"), (8, "C4")])
 def test_bench_ranks_gloo_one_gpu(tmp_path, cornell_scene, world, config):
     W, Hh, spp, chunk = 160, 90, 6, 3
     out = str(tmp_path / "frame.npy")
@@ -38,11 +38,31 @@ def test_bench_ranks_gloo_one_gpu(tmp_path, cornell_scene, world, config):
            "--config", config, "--dist-backend", "gloo", "--width", str(W), "--height", str(Hh), "--spp", str(spp),
            "--chunk", str(chunk), "--steps", "1", "--warmup", "1", "--no-cold", "--no-cpu-baseline",
            "--dump-frame", out]
-    r = subprocess.run(cmd, cwd=REPO, env=env, capture_output=True, text=True, timeout=300)
+    tj = None
+    if world == 2:
+        # rank 0's share carries a roofline when a PMC summary of that share (same build, world
+        # recorded) is given: a synthetic one here -- the plumbing, not the counters
+        import hashlib
+        import json
+        with open(H.LIB_PATH, "rb") as fh:
+            sha = hashlib.sha256(fh.read()).hexdigest()
+        tj = str(tmp_path / "C2_w2.json")
+        with open(tj, "w") as fh:
+            json.dump({"scene": "cornell", "width": W, "height": Hh, "chunk": chunk, "world": 2, "lib_sha256": sha,
+                       "clock_ghz": 2.4, "counters_per_launch": {"SQ_INSTS_VALU": 1e6, "GRBM_GUI_ACTIVE": 8e6,
+                                                                 "SQ_WAVE_CYCLES": 1e6}}, fh)
+        cmd += ["--traffic-json", tj]
+    r = subprocess.run(cmd, cwd=REPO, env=env, capture_output=True, text=True, timeout=420)
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
+    if tj:
+        import json
+        line = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
+        rf = line["roofline"]
+        assert rf["frac"] is not None and rf["bound"] == "valu" and "rank 0" in rf["share"], rf
     img = np.load(out)
     import pt_scenes
-    sc = cornell_scene if config == "C2" else H.setupBuffers(*pt_scenes.write_scene("bunny", os.path.join(REPO, "scenes")))
+    name = {"C3": "bunny", "C4": "sponza"}.get(config)
+    sc = cornell_scene if name is None else H.setupBuffers(*pt_scenes.write_scene(name, os.path.join(REPO, "scenes")))
     pt = H.PathTracer(W, Hh, max_bounce=8)
     pt.upload(sc)
     pt.render(1, spp, 0)

@@ -114,3 +114,21 @@ def test_wide_key_validation(cornell_scene):
     pt.set_key(16, 1)
     pt.set_key(16, 0)
     pt.close()
+
+
+def test_orphan_leaf_node_is_skipped(cornell_scene):
+    """A leaf record no link from the root reaches (appended to a nested tree) is accepted by
+    pt_upload_scene (links are checked on every node, cycles from the root).  The wide tree
+    gives it no index, and the upload must not place its triangles (it used to write before the
+    wide triangle array); the image is the oracle's, on the wide global walk (variant 3)."""
+    sc = dict(cornell_scene)
+    nodes = np.asarray(sc["nodes"], np.float32).reshape(-1, 12)
+    leaf = next(i for i in range(len(nodes)) if nodes[i, 8] > -1.0)
+    orphan = nodes[leaf].copy()
+    orphan[10] = orphan[11] = -1.0
+    sc["nodes"] = np.concatenate([nodes, orphan[None]], axis=0)
+    W, Hh = 96, 72
+    want = O.render(cornell_scene, W, Hh, max_bounce=8, n_frames=3)
+    for variant in (3, 0):
+        got = render(sc, W, Hh, 3, variant=variant)
+        assert_bitwise(got, want, "orphan leaf, variant %d" % variant)

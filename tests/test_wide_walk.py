@@ -46,6 +46,8 @@ def sim(tmp_path_factory):
 
 def _ok(res):
     assert res["rc"] == 0 and res["mismatches"] == 0 and res["cons_violations"] == 0, res["stderr"][:2000]
+    # every retest the leaf certificate skips (pt_wide.h) would have passed the exact test
+    assert res["cert_violations"] == 0, res["stderr"][:2000]
 
 
 def test_cornell(sim, cornell_scene):
@@ -91,3 +93,21 @@ def test_single_leaf_and_two_leaf_trees(sim):
         sc = H.scene_from_arrays(tris, mats)
         sc["cam"] = np.array([0.5, -6, 0.5, 0, 0.1, 1, 0.05, 0, 0, 0, 0, 0], np.float32)
         _ok(sim(sc, stride=64, adversarial=4000))
+
+
+@pytest.mark.parametrize("seed", [1, 2, 3])
+def test_leaf_certificate_fuzz(tmp_path, seed):
+    """ptw::leaf_certificate against the reference's exact slab test of the leaf box
+    (tests/wide/cert_fuzz.cpp): rays aimed at vertices, edges and interior points of leaf
+    triangles (nudged a few ulps), flat axis-aligned leaves among them, near and far origins;
+    for every hit that could move t, a certified hit must pass the exact test at t just above
+    t_h and beyond.  The sample is adversarial (tens of thousands of exact-test failures);
+    none may be certified, and most ordinary hits certify."""
+    exe = str(tmp_path / "cert_fuzz")
+    subprocess.check_call(["g++", "-O2", "-std=c++17", "-ffp-contract=off", "-march=x86-64-v3", "-o", exe,
+                           os.path.join(REPO, "tests", "wide", "cert_fuzz.cpp")])
+    r = subprocess.run([exe, "3000000", str(seed)], capture_output=True, text=True)
+    out = json.loads(r.stdout.strip().splitlines()[-1])
+    assert r.returncode == 0 and out["violations"] == 0, r.stderr[:2000]
+    assert out["exact_fail"] > 1000                   # the sample does reach the failing cases
+    assert out["certified"] > 0.8 * out["hits"] and out["flat_certified"] > 0.7 * out["flat_hits"]

@@ -113,7 +113,8 @@ RefOut ref_walk(f3 o, f3 d, float t0) {
 
 ptw::WideTree W;
 long cons_violations = 0;
-struct WideOut { float t; int tri; long visits, resumes, leaves, retests, retest_fail, pops, top_visits, lines; };
+struct WideOut { float t; int tri; long visits, resumes, leaves, retests, retest_fail, pops, top_visits, lines, certified; };
+long cert_violations = 0;
 
 // the exact-reciprocal guard, ray half
 bool in_guard(f3 o, f3 d) {
@@ -125,7 +126,7 @@ bool in_guard(f3 o, f3 d) {
 int top_records = 512;   // indices below this are staged in LDS by the kernel
 
 WideOut wide_walk(f3 o, f3 d, float t0) {
-    WideOut r{t0, -1, 0, 0, 0, 0, 0, 0, 0, 0};
+    WideOut r{t0, -1, 0, 0, 0, 0, 0, 0, 0, 0, 0};
     const f3 rd = mk(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
     const ptw::WRay wr = ptw::make_wray(o, rd, W.cw, std::signbit(d.x), std::signbit(d.y), std::signbit(d.z));
     int cur = 0, R = -1;
@@ -165,7 +166,16 @@ WideOut wide_walk(f3 o, f3 d, float t0) {
             r.retests++;
             const float* lb = &W.lbox[(size_t)g * 8];
             const float lo[3] = {lb[0], lb[2], lb[4]}, hi[3] = {lb[1], lb[3], lb[5]};
-            if (slab_exact(lo, hi, o, d, r.t)) { r.t = t2; r.tri = tri; }
+            const bool exact = slab_exact(lo, hi, o, d, r.t);
+            const float* tr = &tris[16 * (size_t)tri];
+            const f3 p = o + d * t2;
+            const f3 v0 = ld3(tr), v1 = ld3(tr + 4), v2 = ld3(tr + 8);
+            const f3 n = pt::normalize(pt::cross(v1 - v0, v2 - v0));
+            if (ptw::leaf_certificate(p, n, v0, v1, v2, ptw::abs_max3(o))) {
+                r.certified++;
+                if (!exact) cert_violations++;
+            }
+            if (exact) { r.t = t2; r.tri = tri; }
             else r.retest_fail++;
         }
         r.pops++;
@@ -174,7 +184,7 @@ WideOut wide_walk(f3 o, f3 d, float t0) {
     return r;
 }
 
-struct Acc { double segs = 0, rv = 0, rl = 0, wv = 0, wr = 0, wl = 0, wt = 0, wf = 0, top = 0, lines = 0, ref_top = 0; };
+struct Acc { double segs = 0, rv = 0, rl = 0, wv = 0, wr = 0, wl = 0, wt = 0, wf = 0, top = 0, lines = 0, ref_top = 0, wc = 0; };
 
 long mismatches = 0, slow = 0;
 void segment(f3 o, f3 d, Acc& A, float* t_out, int* tri_out) {
@@ -204,6 +214,7 @@ void segment(f3 o, f3 d, Acc& A, float* t_out, int* tri_out) {
     A.wf += wo.retest_fail;
     A.top += wo.top_visits;
     A.lines += wo.lines;
+    A.wc += wo.certified;
 }
 
 }  // namespace
@@ -308,8 +319,8 @@ int main(int argc, char** argv) {
                 "\"path_segments\": %.0f, \"slow\": %ld, \"mismatches\": %ld, \"cons_violations\": %ld, "
                 "\"ref_visits\": %.3f, \"ref_leaves\": %.3f, \"ref_top\": %.3f, \"wide_visits\": %.3f, \"wide_resumes\": %.3f, "
                 "\"wide_leaves\": %.3f, \"wide_retests\": %.3f, \"wide_retest_fail\": %.4f, \"wide_top\": %.3f, "
-                "\"wide_lines\": %.3f}\n",
+                "\"wide_lines\": %.3f, \"wide_certified\": %.4f, \"cert_violations\": %ld}\n",
                 nt, nn, W.n_records, W.n_index, W.depth, A.segs, path_segs, slow, mismatches, cons_violations,
-                A.rv / A.segs, A.rl / A.segs, A.ref_top / A.segs, A.wv / s, A.wr / s, A.wl / s, A.wt / s, A.wf / s, A.top / s, A.lines / s);
-    return (mismatches || cons_violations) ? 1 : 0;
+                A.rv / A.segs, A.rl / A.segs, A.ref_top / A.segs, A.wv / s, A.wr / s, A.wl / s, A.wt / s, A.wf / s, A.top / s, A.lines / s, A.wc / s, cert_violations);
+    return (mismatches || cons_violations || cert_violations) ? 1 : 0;
 }

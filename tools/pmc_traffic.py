@@ -1,12 +1,18 @@
-"""Reduce rocprofv3 PMC passes (tools/gpu_pmc.sh output) for the render launch.
+"""Reduce rocprofv3 PMC passes (tools/gpu_pmc.sh output) for the render launch of one bench
+configuration.
+
+python tools/pmc_traffic.py gpurun_out/pmc/C3 r05a C3 [world=N]
 
 A render launch is the state-machine kernel plus, in the frame-split mode, the k_accum_frames
 pass that follows it; counters are summed over both and averaged over launches (the first,
-warm-up launch dropped).  Writes profiles/<tag>_pmc.json and profiles/traffic_latest.json:
+warm-up launch dropped).  Writes profiles/pmc/<config>[_wN].json (what bench.py reads) and the
+per-round copy profiles/<tag>_pmc_<config>[_wN].json:
   hbm_bytes_per_launch = 2 * FETCH_SIZE * 1024 + WRITE_SIZE * 1024, per render launch.
 The factor 2 on FETCH_SIZE is the gfx950 correction of MI355X_MICROARCH.md §HBM (FETCH_SIZE
 reports half the bytes of wide 16-B/lane reads; the accumulator and colour-buffer reads are
 float4 per lane); WRITE_SIZE is exact for 16-B/lane stores.  Raw values are kept alongside.
+The summary records the sha256 of the library it profiled: bench.py uses it only for that
+build and workload (bench.pmc_for).
 """
 import collections
 import csv
@@ -16,6 +22,7 @@ import os
 import sys
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, REPO)
 
 
 def load(d):
@@ -43,13 +50,7 @@ def load(d):
     return launches
 
 
-def main():
-    pmc = sys.argv[1] if len(sys.argv) > 1 else os.path.join(REPO, "gpurun_out", "pmc")
-    tag = sys.argv[2] if len(sys.argv) > 2 else "latest"
-    meta = dict(scene="cornell", width=1920, height=1080, chunk=1024)
-    for a in sys.argv[3:]:
-        k, v = a.split("=")
-        meta[k] = int(v) if v.isdigit() else v
+def reduce(pmc, meta):
     out = dict(meta)
     per = collections.defaultdict(list)
     for name in sorted(os.listdir(pmc)):
@@ -57,8 +58,7 @@ def main():
         if not os.path.isdir(d) or not os.path.exists(os.path.join(d, "run_counter_collection.csv")):
             continue
         launches = load(d)
-        # full-size launches only (a cold first render starts with a 2-frame probe launch),
-        # then drop the warm-up render when possible
+        # full-size launches only, then drop the warm-up render when possible
         top = max(sum(ms.values()) for _, ms in launches)
         launches = [(ctr, ms) for ctr, ms in launches if sum(ms.values()) >= 0.5 * top]
         for ctr, ms in (launches[1:] or launches):
@@ -69,7 +69,6 @@ def main():
                 per["%s_ms_%s" % (kind, name)].append(v)
     avg = {k: sum(v) / len(v) for k, v in per.items()}
     out["counters_per_launch"] = avg
-    # the build these counters belong to: bench.py uses them only for this exact library
     lib = os.path.join(REPO, "opengl-path-tracing_amd", "build", "libptrace.so")
     with open(lib, "rb") as fh:
         out["lib_sha256"] = hashlib.sha256(fh.read()).hexdigest()
@@ -80,22 +79,44 @@ def main():
         out["fetch_bytes_raw"] = avg["FETCH_SIZE"] * 1024
         out["write_bytes"] = avg["WRITE_SIZE"] * 1024
         out["hbm_bytes_per_launch"] = 2 * avg["FETCH_SIZE"] * 1024 + avg["WRITE_SIZE"] * 1024
+    if "GRBM_GUI_ACTIVE" in avg:
+        # GRBM_GUI_ACTIVE sums the 8 XCDs' busy clocks; the clock is held over the launch
+        cycles = avg["GRBM_GUI_ACTIVE"] / 8.0
+        pass_ms = [avg[k] for k in ("launch_ms_sq2", "launch_ms_mem", "launch_ms_l2") if k in avg]
+        out["clock_ghz"] = cycles / (pass_ms[0] * 1e6)
+        if "SQ_INSTS_VALU" in avg:
+            # a wave64 VALU op holds a SIMD-32 for 2 cycles (MI355X_MICROARCH.md); 1024 SIMDs
+            out["valu_busy_frac"] = 2.0 * avg["SQ_INSTS_VALU"] / (1024.0 * cycles)
+            out["valu_instr_per_launch"] = avg["SQ_INSTS_VALU"]
+        if "TD_TD_BUSY_sum" in avg:
+            out["td_busy_frac"] = avg["TD_TD_BUSY_sum"] / (256.0 * cycles)
+        if "SQ_WAVE_CYCLES" in avg:
+            out["waves_per_simd"] = 4.0 * avg["SQ_WAVE_CYCLES"] / (1024.0 * cycles)
     if "SQ_THREAD_CYCLES_VALU" in avg:
         out["valu_active_lanes_per_instr"] = avg["SQ_THREAD_CYCLES_VALU"] / max(avg["SQ_ACTIVE_INST_VALU"], 1)
-    if "SQ_INSTS_VALU" in avg and "GRBM_GUI_ACTIVE" in avg:
-        # VALU pipe occupancy: a wave64 VALU op holds a SIMD-32 for 2 cycles (MI355X_MICROARCH.md);
-        # GRBM_GUI_ACTIVE sums the 8 XCDs' busy clocks; 256 CUs x 4 SIMDs.
-        cycles = avg["GRBM_GUI_ACTIVE"] / 8.0
-        out["valu_busy_frac"] = 2.0 * avg["SQ_INSTS_VALU"] / (1024.0 * cycles)
-        out["clock_ghz"] = cycles / (avg.get("launch_ms_sq2", avg.get("launch_ms_sq1", 1.0)) * 1e6)
-        out["valu_instr_per_launch"] = avg["SQ_INSTS_VALU"]
-        out["source"] = "profiles/%s_pmc.json (rocprofv3 --pmc passes of tools/pmc_run.py, same workload)" % tag
+    if "TCC_HIT_sum" in avg:
+        out["l2_hit_rate"] = avg["TCC_HIT_sum"] / max(avg["TCC_HIT_sum"] + avg["TCC_MISS_sum"], 1.0)
     if "SQ_WAVE_CYCLES" in avg and "SQ_WAIT_ANY" in avg:
         tot = avg["SQ_WAVE_CYCLES"]
         out["wave_cycle_split"] = {k: avg[k] / tot for k in ("SQ_ACTIVE_INST_ANY", "SQ_WAIT_INST_ANY", "SQ_WAIT_ANY") if k in avg}
-    os.makedirs(os.path.join(REPO, "profiles"), exist_ok=True)
-    for fn in ("%s_pmc.json" % tag, "traffic_latest.json"):
-        with open(os.path.join(REPO, "profiles", fn), "w") as fh:
+    return out
+
+
+def main():
+    pmc, tag, cfg = sys.argv[1], sys.argv[2], sys.argv[3]
+    import bench
+    scene, W, H, spp, bounces, chunk0, graph = bench.CONFIGS[cfg]
+    meta = dict(config=cfg, scene=scene, width=W, height=H, world=1)
+    for a in sys.argv[4:]:
+        k, v = a.split("=")
+        meta[k] = int(v) if v.isdigit() else v
+    meta["chunk"] = min(meta.get("chunk") or (chunk0 * meta["world"] if graph == 0 else chunk0), spp)
+    out = reduce(pmc, meta)
+    name = cfg if meta["world"] == 1 else "%s_w%d" % (cfg, meta["world"])
+    out["source"] = "profiles/%s_pmc_%s.json (rocprofv3 --pmc passes of tools/pmc_run.py, same workload)" % (tag, name)
+    os.makedirs(os.path.join(REPO, "profiles", "pmc"), exist_ok=True)
+    for fn in (os.path.join("profiles", "%s_pmc_%s.json" % (tag, name)), os.path.join("profiles", "pmc", "%s.json" % name)):
+        with open(os.path.join(REPO, fn), "w") as fh:
             json.dump(out, fh, indent=1, sort_keys=True)
     print(json.dumps({k: v for k, v in out.items() if k != "counters_per_launch"}, indent=1))
 
