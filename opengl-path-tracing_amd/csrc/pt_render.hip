@@ -401,7 +401,7 @@ __device__ __forceinline__ float tri_plane(float4 nd, f3 o, f3 d) {    // nd: qu
 // from the plane test (quad 0), so only the vertices (quads 1-3) are read.
 // With `cert_on` (wave-uniform) it also evaluates the leaf re-test certificate of this
 // triangle at p (ptw::leaf_certificate, pt_wide.h): its vertices are at hand here.
-template <bool LDS>
+template <bool LDS, bool CERT>
 __device__ __forceinline__ bool tri_edges_at(const SceneView& S, int slot, f3 n, f3 p, bool cert_on, float omax,
                                              bool& cert) {
     const float4 q1 = tri_quad<LDS>(S, slot, 1), q2 = tri_quad<LDS>(S, slot, 2), q3 = tri_quad<LDS>(S, slot, 3);
@@ -409,7 +409,7 @@ __device__ __forceinline__ bool tri_edges_at(const SceneView& S, int slot, f3 n,
     const float e0 = pt::dot(n, pt::cross(v1 - v0, p - v0));
     const float e1 = pt::dot(n, pt::cross(v2 - v1, p - v1));
     const float e2 = pt::dot(n, pt::cross(v0 - v2, p - v2));
-    if (cert_on) cert = ptw::leaf_certificate(p, n, v0, v1, v2, omax);
+    if (CERT && cert_on) cert = ptw::leaf_certificate(p, n, v0, v1, v2, omax);
     return (e0 > 0.0f) & (e1 > 0.0f) & (e2 > 0.0f);
 }
 // The lane's index in its wave, recomputed where it is used (two VALU): a value held across
@@ -444,7 +444,7 @@ __device__ __forceinline__ float fperm_f(int dst_bytes, float v) {
 // nda: quad 0 {n, d0} of slot s0; cop: the leaf code's coplanar bit.
 // cert_on (wave-uniform): also return each triangle's leaf re-test certificate (ca / cb, for
 // a triangle whose edge tests pass; omax = max_i |o_i|), computed by the lane that tests it.
-template <bool LDS>
+template <bool LDS, bool CERT>
 __device__ __forceinline__ void leaf_pair_tests(const SceneView& S, bool at, int s0, float4 nda, bool cop,
                                                 f3 o, f3 d, float t, int max_pairs, float& h1, float& h2,
                                                 bool cert_on, bool& cta, bool& ctb) {
@@ -497,22 +497,22 @@ __device__ __forceinline__ void leaf_pair_tests(const SceneView& S, bool at, int
         }
         bool pass = false, cert = false;
         float wom = 0.0f;
-        if (cert_on) {
+        if (CERT && cert_on) {
             const float oa = fperm_f(da, omax), ob = fperm_f(db, omax);
             wom = first ? oa : ob;
         }
-        if (lane < n) pass = tri_edges_at<LDS>(S, ws, wn, wp, cert_on, wom, cert);
+        if (lane < n) pass = tri_edges_at<LDS, CERT>(S, ws, wn, wp, cert_on, wom, cert);
         const unsigned long long r = __ballot(pass);
         oka = na & (((r >> ja) & 1ull) != 0ull);
         okb = nb & (((r >> jb) & 1ull) != 0ull);
-        if (cert_on) {
+        if (CERT && cert_on) {
             const unsigned long long rc = __ballot(pass & cert);
             cta = oka & (((rc >> ja) & 1ull) != 0ull);
             ctb = okb & (((rc >> jb) & 1ull) != 0ull);
         }
     } else {
-        if (na) oka = tri_edges_at<LDS>(S, s0, na3, o + d * ta, cert_on, omax, cta);
-        if (nb) okb = tri_edges_at<LDS>(S, s0 + 1, nb3, o + d * tb, cert_on, omax, ctb);
+        if (na) oka = tri_edges_at<LDS, CERT>(S, s0, na3, o + d * ta, cert_on, omax, cta);
+        if (nb) okb = tri_edges_at<LDS, CERT>(S, s0 + 1, nb3, o + d * tb, cert_on, omax, ctb);
         cta = cta & oka;
         ctb = ctb & okb;
     }
@@ -1181,7 +1181,7 @@ __global__ __launch_bounds__(NT, MINW) void k_render_sm(KParams p) {
                                 tri_quad<LDS>(S, s0 + 1, 3), o, d);
                 }
             } else {
-                leaf_pair_tests<LDS>(S, at, s0, nd0, cop, o, d, t, p.compact_max, h1, h2, p.leaf_cert != 0, ca, cb);
+                leaf_pair_tests<LDS, WIDE>(S, at, s0, nd0, cop, o, d, t, p.compact_max, h1, h2, WIDE && p.leaf_cert != 0, ca, cb);
             }
             bool c1 = false, c2 = false;
             if (at) {
@@ -1934,6 +1934,7 @@ int pt_upload_scene(pt_ctx* c, const float* tris, int n_tris, const float* bvh, 
             std::memcpy(&dnw[2 * (size_t)pos[i] + 1].z, &a, 4);
             put_tri(&dtw[8 * (size_t)g], t0);
             put_tri(&dtw[8 * (size_t)g + 4], t1);
+
         }
     }
     HIPCHK(c, hipStreamSynchronize(c->stream));   // a render in flight may still read the old scene
@@ -2380,7 +2381,9 @@ static int enqueue_render(pt_ctx* c, int frame_first, int n_frames, int acc_firs
     p.n_mats = c->n_mats;
     p.scene_fast = c->scene_fast;
     p.cons_walk = cons_walk_on(c);
-    // the certificate stands on hit_triangle's plane distance: not in Moller-Trumbore mode
+    // the certificate stands on hit_triangle's plane distance: not in Moller-Trumbore mode.
+    // The wide walk only: on the LDS culling walk (C2, VALU-bound, the box re-read from LDS)
+    // its ~40 VALU per leaf phase cost more than the re-test (-1.9%, same-process A/B r05c)
     p.leaf_cert = c->leaf_cert_ok && !c->cert_off && !(c->cfg.flags & PT_FLAG_MOLLER_TRUMBORE);
     p.sc.walk_sk = c->d_walk_sk;
     std::memcpy(p.cons_m, c->cons_m, sizeof(p.cons_m));
@@ -2470,6 +2473,7 @@ static int enqueue_render(pt_ctx* c, int frame_first, int n_frames, int acc_firs
     // key 16 turns it off; counting builds keep the binary walk (their counts are the
     // reference's), and so do occupancy overrides other than 6 waves per SIMD
     const bool use_wide = !use_lds && wide_walk_on(c);
+    p.leaf_cert = p.leaf_cert && use_wide;
     if (use_wide) {
         p.sc.nodes = c->d_nodesw;
         p.sc.tris = c->d_trisw;

@@ -7,6 +7,7 @@
 #include <array>
 #include <cmath>
 #include <cstring>
+#include <functional>
 
 namespace ptw {
 namespace {
@@ -16,6 +17,13 @@ namespace {
 #endif
 constexpr int kWideOrder = PT_WIDE_ORDER;   // group numbering below the top (see wide_build)
 constexpr int kTopBreadth = 4096;           // indices numbered breadth-first first (>= any LDS top)
+#ifndef PT_WIDE_COLLAPSE
+#define PT_WIDE_COLLAPSE 0
+#endif
+constexpr int kWideCollapse = PT_WIDE_COLLAPSE;   // frontier choice (see wide_build)
+// (every leaf is a member of exactly one cut, so its cost term is the same for every cut:
+// only the record visits, weighted by area, decide)
+constexpr double kCostRec = 1.0, kCostLeaf = 1.0;
 
 struct BN {
     float lo[3], hi[3];
@@ -114,10 +122,67 @@ int wide_build(const float* bvh, int n_nodes, const unsigned char* leaf_cop, Wid
             st.push_back(l);
         }
     }
+    // PT_WIDE_COLLAPSE 1: each record's frontier is the cut of its binary subtree that
+    // minimises the surface-area cost (a record visit costs kCostRec, a leaf kCostLeaf, each
+    // weighted by its box area over the record's), by dynamic programming over the subtree,
+    // bottom-up: F[y][k] = least cost of covering subtree y with at most k members.
+    std::vector<std::array<double, 5>> F;
+    std::vector<std::array<signed char, 5>> split;   // 0: y itself is the member; k1: l gets k1
+    if (kWideCollapse == 1) {
+        F.assign(n_nodes, {0, 0, 0, 0, 0});
+        split.assign(n_nodes, {0, 0, 0, 0, 0});
+        std::vector<int> order, st{0};
+        while (!st.empty()) {               // preorder; reversed it is a valid bottom-up order
+            const int x = st.back();
+            st.pop_back();
+            order.push_back(x);
+            if (!bn[x].leaf) { st.push_back(bn[x].left); st.push_back(bn[x].right); }
+        }
+        for (auto it = order.rbegin(); it != order.rend(); ++it) {
+            const int y = *it;
+            const double a = area(bn[y]) + 1e-30;
+            if (bn[y].leaf) {
+                for (int k = 1; k <= 4; k++) F[y][k] = a * kCostLeaf;
+                continue;
+            }
+            const int l = bn[y].left, r = bn[y].right;
+            double best = 1e300;                  // y as a record: its own best cut below
+            for (int k1 = 1; k1 <= 3; k1++) best = std::min(best, F[l][k1] + F[r][4 - k1]);
+            const double own = a * kCostRec + best;   // = a * C(y)
+            F[y][1] = own;
+            for (int k = 2; k <= 4; k++) {
+                F[y][k] = F[y][k - 1];
+                split[y][k] = split[y][k - 1];
+                if (k == 2 && own <= F[y][k]) split[y][k] = 0;
+                for (int k1 = 1; k1 < k; k1++) {
+                    const double c = F[l][k1] + F[r][k - k1];
+                    if (c < F[y][k]) { F[y][k] = c; split[y][k] = (signed char)k1; }
+                }
+            }
+        }
+    }
+    // expands subtree y into at most k members (PT_WIDE_COLLAPSE 1), in preorder
+    std::function<void(int, int, int*, int&)> expand = [&](int y, int k, int* f, int& n) {
+        const int k1 = bn[y].leaf ? 0 : split[y][k];
+        if (k1 == 0) { f[n++] = y; return; }
+        expand(bn[y].left, k1, f, n);
+        expand(bn[y].right, k - k1, f, n);
+    };
     // record frontiers: [left, right], then the internal member of largest surface area
     // replaced by its two children (in place: the list stays in preorder) until 4 members
     auto frontier = [&](int x, int* f) {
         if (bn[x].leaf) { f[0] = x; return 1; }   // a root leaf: a record with that one child
+        if (kWideCollapse == 1) {
+            const int l = bn[x].left, r = bn[x].right;
+            int bk = 1;
+            double best = 1e300;
+            for (int k1 = 1; k1 <= 3; k1++)
+                if (F[l][k1] + F[r][4 - k1] < best) { best = F[l][k1] + F[r][4 - k1]; bk = k1; }
+            int n = 0;
+            expand(l, bk, f, n);
+            expand(r, 4 - bk, f, n);
+            return n;
+        }
         int n = 2;
         f[0] = bn[x].left;
         f[1] = bn[x].right;
@@ -174,6 +239,25 @@ int wide_build(const float* bvh, int n_nodes, const unsigned char* leaf_cop, Wid
         nkids[ri] = n;
     };
     size_t qi = 0;
+    if (kWideOrder == 3) {
+        // best-first: the pending record of largest box area (the likeliest to be visited by
+        // an incoherent ray) has its group allocated next, so the first indices -- the ones
+        // the kernel stages in LDS -- hold the most visited records
+        std::vector<std::pair<double, int>> heap{{area(bn[recs[0]]), 0}};
+        std::vector<int> found;
+        while (!heap.empty() && !overflow) {
+            std::pop_heap(heap.begin(), heap.end());
+            const int ri = heap.back().second;
+            heap.pop_back();
+            found.clear();
+            process((size_t)ri, &found);
+            for (int c : found) {
+                heap.emplace_back(area(bn[recs[c]]), c);
+                std::push_heap(heap.begin(), heap.end());
+            }
+        }
+        qi = recs.size();
+    }
     for (; qi < recs.size() && (kWideOrder == 0 || next < kTopBreadth) && !overflow; qi++) process(qi, nullptr);
     const size_t pending = recs.size();
     for (size_t r0 = qi; r0 < pending && !overflow; r0++) {   // the subtrees below the breadth-first top

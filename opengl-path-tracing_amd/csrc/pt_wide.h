@@ -127,36 +127,38 @@ PT_HD uint32_t wide_hits(float ox, float oy, float oz, uint32_t w, uint32_t a0, 
     return (w >> 24) & hit & ((0xffu << (2 * s)) & 0xffu);
 }
 
-// The leaf re-test certificate (DESIGN.md §5.10).  A leaf reached on the conservative test
+// The leaf re-test certificate (DESIGN.md §5.11).  A leaf reached on the conservative test
 // must pass the reference's exact slab test of its own box at the current t before one of
 // its triangles may move t (computeShader.c:406-428 tests the leaf only then).  When the
 // leaf's box contains the hit triangle's vertices (pt_upload_scene checks every leaf; the
-// reference builder expands leaf boxes over them, bvh.h:29-52) and the hit point
-// p = o + d*t_h (componentwise RN(o_i + RN(d_i t_h)), as the kernel forms it) lies inside the
-// triangle's vertex box [m, M] by g = 2^-20 (|p_i| + |m_i or M_i| + max_j |o_j|) + 2^-100 on
-// every axis, the exact test passes at any t > t_h, so the re-test can be skipped:
-//   RN(p_i - m_i) >= g gives, through |p - (o + s)| <= 2^-23 |p|, |s - d t_h| <= 2^-23 |s|
-//   (s = RN(d_i t_h)) and |RN(m - o) - (m - o)| <= 2^-24 |m - o|, that RN(m_i - o_i) <= d_i t_h,
-//   and RN(lo_i - o_i) <= RN(m_i - o_i) (lo_i <= m_i); likewise d_i t_h <= RN(hi_i - o_i).
-//   Then for either sign of d_i the near quotient RN(RN(b - o)/d) of axis i is <= t_h and
-//   the far one >= t_h (RN is monotone and t_h is a float), so max near <= t_h <= min far,
-//   and t_h < t.  The needed margin is below 2^-22 (|p| + |m| + |o|); g is four times that.
-// Axis i on which the hit triangle is flat (v0_i = v1_i = v2_i = c) with a stored normal of
-// exactly +-1 there (the other two components are then exact zeros): the plane distance
-// -(dot(n, o) + d0) / dot(n, d) (computeShader.c:285-297) is bit for bit RN(RN(c - o_i) / d_i),
-// the reference's slab quotient of the plane c, and with lo_i <= c <= hi_i monotonicity gives
-// near_i <= t_h <= far_i for either sign of d_i -- no margin needed on that axis.
+// reference builder expands leaf boxes over them, bvh.h:29-52), each axis i is certified by
+// one of:
+//   margin: for the triangle's vertex interval [m_i, M_i] and the hit point p = o + d*t_h
+//   (componentwise RN(o_i + RN(d_i t_h)), as the kernel forms it), if RN(p_i - m_i) and
+//   RN(M_i - p_i) both clear g = 2^-20 (max_j |p_j| + max_j |o_j|) + 2^-100, then through |p - (o + s)| <=
+//   2^-23 |p|, |s - d t_h| <= 2^-23 |s| (s = RN(d_i t_h)), |RN(m - o) - (m - o)| <= 2^-24 |m - o|
+//   and |m_i| <= |p_i| + (p_i - m_i), RN(m_i - o_i) <= d_i t_h <= RN(M_i - o_i); the leaf box
+//   contains the triangle (lo_i <= m_i, M_i <= hi_i), so RN(lo_i - o_i) <= d_i t_h <=
+//   RN(hi_i - o_i), and for either sign of d_i RN's monotonicity puts the reference's near
+//   quotient RN(RN(b - o)/d) of axis i at or below t_h and the far one at or above it (t_h is
+//   a float).  The margin needed is below 2^-21.9 (|p_i| + |o|); g is about four times that.
+//   exact axis plane: the triangle is flat on axis i (v0_i = v1_i = v2_i = c) and its stored
+//   normal is exactly +-1 there (its other components are then exact zeros): the plane
+//   distance -(dot(n, o) + d0) / dot(n, d) (computeShader.c:285-297) is bit for bit
+//   RN(RN(c - o_i) / d_i), the reference's slab quotient of the plane c, and lo_i <= c <= hi_i
+//   gives near_i <= t_h <= far_i for either sign of d_i.
+// All three axes certified: max near <= t_h <= min far and t_h < t, so the exact test passes.
 PT_HD float abs_max3(pt::f3 v) { return fmaxf(fmaxf(__builtin_fabsf(v.x), __builtin_fabsf(v.y)), __builtin_fabsf(v.z)); }
-PT_HD bool cert_axis(float p, float a, float b, float c, float n, float omax) {
+// Axis i: m, M = the triangle's vertex interval; RN(p - m) and RN(M - p) against g (the margin
+// form), or m == M with |n_i| == 1 (the exact axis plane form).
+PT_HD bool cert_axis(float p, float a, float b, float c, float n, float g) {
     const float m = fminf(fminf(a, b), c), M = fmaxf(fmaxf(a, b), c);
-    const float ap = __builtin_fabsf(p);
-    const float gl = 0x1p-20f * ((ap + __builtin_fabsf(m)) + omax) + 0x1p-100f;
-    const float gh = 0x1p-20f * ((ap + __builtin_fabsf(M)) + omax) + 0x1p-100f;
-    return ((p - m >= gl) & (M - p >= gh)) | ((m == M) & (__builtin_fabsf(n) == 1.0f));
+    return ((p - m >= g) & (M - p >= g)) | ((m == M) & (__builtin_fabsf(n) == 1.0f));
 }
 PT_HD bool leaf_certificate(pt::f3 p, pt::f3 n, pt::f3 v0, pt::f3 v1, pt::f3 v2, float omax) {
-    return cert_axis(p.x, v0.x, v1.x, v2.x, n.x, omax) & cert_axis(p.y, v0.y, v1.y, v2.y, n.y, omax) &
-           cert_axis(p.z, v0.z, v1.z, v2.z, n.z, omax);
+    const float g = 0x1p-20f * (abs_max3(p) + omax) + 0x1p-100f;
+    return cert_axis(p.x, v0.x, v1.x, v2.x, n.x, g) & cert_axis(p.y, v0.y, v1.y, v2.y, n.y, g) &
+           cert_axis(p.z, v0.z, v1.z, v2.z, n.z, g);
 }
 
 // The next position from the stack (K entries, e[0] the top), or from R once it is empty.

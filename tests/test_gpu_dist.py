@@ -70,3 +70,28 @@ def test_bench_ranks_gloo_one_gpu(tmp_path, cornell_scene, world, config):
     pt.close()
     assert img.shape == want.shape
     assert_bitwise(img, want, "%d-rank bench frame vs one context" % world)
+
+
+def test_bench_share_proxy_line(tmp_path):
+    """bench.py --share-of N: one process renders rank 0's share of an N-way row split with no
+    collective (the per-GPU proxy of the configs BASELINE sends to 8 GPUs); the line says so
+    and its frame rows are rank 0's (y = 0 mod N)."""
+    import json
+    W, Hh, spp = 96, 40, 4
+    out = str(tmp_path / "frame.npy")
+    cmd = [sys.executable, "bench.py", "--config", "C2", "--share-of", "4", "--width", str(W), "--height", str(Hh),
+           "--spp", str(spp), "--chunk", "2", "--steps", "1", "--warmup", "1", "--no-cold", "--no-cpu-baseline",
+           "--dump-frame", out]
+    r = subprocess.run(cmd, cwd=REPO, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    line = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
+    assert line["n_gpus"] == 1 and line["share_proxy"]["of"] == 4 and line["share_proxy"]["rows"] == 10
+    assert line["value"] > 0 and "share proxy" in line["config"]["parallelism"]
+    img = np.load(out)                          # rank 0's rows_local x W accumulation
+    pt = H.PathTracer(W, Hh, max_bounce=8)
+    import pt_scenes
+    pt.upload(H.setupBuffers(*pt_scenes.write_scene("cornell", os.path.join(REPO, "scenes"))))
+    pt.render(1, spp, 0)
+    want = pt.read_rgba32f()
+    pt.close()
+    assert_bitwise(img, want[0::4], "share proxy rows vs one context")
