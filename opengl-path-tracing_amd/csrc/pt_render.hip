@@ -689,10 +689,7 @@ __device__ __forceinline__ void trav_walk(const SceneView& S, f3 o, f3 d, f3 rd,
 // (measured, same-process A/B on the C3 / C4 stand-ins: stack depth 3 and three record visits
 // per yield check with packed 48-B records +3.5% / +3.9% over depth 2, two visits, 64-B
 // stride; each alone +0.5 / +2.6% (depth), +1.3 / -0.2% (unroll), +0.5 / +0.3% (stride))
-#ifndef PT_WIDE_STACK
-#define PT_WIDE_STACK 3
-#endif
-constexpr int kWideStack = PT_WIDE_STACK;
+constexpr int kWideStack = ptw::kStack;   // pt_wide.h (PT_WIDE_STACK)
 // float4 per device record: the three quads of pt_wide.h packed (48 B) or on a 64-B stride
 #ifndef PT_WIDE_STRIDE
 #define PT_WIDE_STRIDE 3
@@ -737,15 +734,7 @@ __device__ __forceinline__ void trav_wide(const SceneView& S, f3 o, f3 rd, float
     for (;;) {
 #pragma unroll
         for (int u = 0; u < PT_WIDE_UNROLL; u++) {
-            bool on = cur >= 0;
-#ifdef PT_WIDE_DEEP_MIN
-            {   // experiment: lanes at global records wait while fewer than PT_WIDE_DEEP_MIN of
-                // them are due and some lane still walks LDS records
-                const bool deep = on & ((cur >> 3) >= S.wtop);
-                const int nd = __popcll(__ballot(deep));
-                if (nd < PT_WIDE_DEEP_MIN && __ballot(on & !deep)) on = on & !deep;
-            }
-#endif
+            const bool on = cur >= 0;
             float4 q0, q1, q2;
             wrec_at(S, on ? cur >> 3 : 0, q0, q1, q2);
             const uint32_t pend = ptw::wide_hits(q0.x, q0.y, q0.z, __float_as_uint(q0.w), __float_as_uint(q1.x),
@@ -1203,23 +1192,14 @@ __global__ __launch_bounds__(NT, MINW) void k_render_sm(KParams p) {
                     }
                 }
             }
-#ifdef PT_EXP_NO_BOXCHK
-            if (false) {   // timing experiment only (not the reference's image)
-#else
             if (WIDE) {
-#endif
                 // the wide walk reached this leaf on the conservative test: as the culling walk,
                 // its own box is tested exactly at this t before a triangle may move t (leaf g's
                 // box at wlbox[2g], [2g + 1]) -- unless the chosen triangle certifies that test
                 const bool chk = at & fast & ((c1 & !ca) | (c2 & !cb));
                 if (__any(chk)) {
                     if (chk) {
-#ifdef PT_WIDE_BOX_IN_REC
-                        const float4* lb = S.wrec + kWideStride * (s0 >> 1);
-                        if (!slab_fast(lb[0], lb[1], o, d, rd, t)) c1 = c2 = false;
-#else
                         if (!slab_fast(S.wlbox[s0], S.wlbox[s0 + 1], o, d, rd, t)) c1 = c2 = false;
-#endif
                     }
                 }
             }

@@ -12,18 +12,12 @@
 namespace ptw {
 namespace {
 
-#ifndef PT_WIDE_ORDER
-#define PT_WIDE_ORDER 0
-#endif
-constexpr int kWideOrder = PT_WIDE_ORDER;   // group numbering below the top (see wide_build)
-constexpr int kTopBreadth = 4096;           // indices numbered breadth-first first (>= any LDS top)
-#ifndef PT_WIDE_COLLAPSE
-#define PT_WIDE_COLLAPSE 0
-#endif
-constexpr int kWideCollapse = PT_WIDE_COLLAPSE;   // frontier choice (see wide_build)
-// (every leaf is a member of exactly one cut, so its cost term is the same for every cut:
-// only the record visits, weighted by area, decide)
-constexpr double kCostRec = 1.0, kCostLeaf = 1.0;
+// Record frontiers (wide_build): the surface-area-optimal cut of each record's binary subtree
+// into at most 4 members.  Every leaf is a member of exactly one cut, so its cost term is the
+// same for every choice of cuts: only the record visits, weighted by area, decide.
+// (Measured against the round-4 greedy frontier -- the member of largest area expanded until
+// four -- with the walk's other settings equal: +0.8% / +1.5% on the C3 / C4 stand-ins.)
+constexpr double kCostRec = 1.0;
 
 struct BN {
     float lo[3], hi[3];
@@ -122,15 +116,12 @@ int wide_build(const float* bvh, int n_nodes, const unsigned char* leaf_cop, Wid
             st.push_back(l);
         }
     }
-    // PT_WIDE_COLLAPSE 1: each record's frontier is the cut of its binary subtree that
-    // minimises the surface-area cost (a record visit costs kCostRec, a leaf kCostLeaf, each
-    // weighted by its box area over the record's), by dynamic programming over the subtree,
-    // bottom-up: F[y][k] = least cost of covering subtree y with at most k members.
-    std::vector<std::array<double, 5>> F;
-    std::vector<std::array<signed char, 5>> split;   // 0: y itself is the member; k1: l gets k1
-    if (kWideCollapse == 1) {
-        F.assign(n_nodes, {0, 0, 0, 0, 0});
-        split.assign(n_nodes, {0, 0, 0, 0, 0});
+    // F[y][k]: least cost of covering subtree y with at most k cut members (a member leaf
+    // costs 0 here, see kCostRec; a member internal node costs area(y) * (kCostRec + its own
+    // best cut's cost)), bottom-up; split[y][k] = how many of the k go left (0: y itself)
+    std::vector<std::array<double, 5>> F(n_nodes, {0, 0, 0, 0, 0});
+    std::vector<std::array<signed char, 5>> split(n_nodes, {0, 0, 0, 0, 0});
+    {
         std::vector<int> order, st{0};
         while (!st.empty()) {               // preorder; reversed it is a valid bottom-up order
             const int x = st.back();
@@ -140,20 +131,14 @@ int wide_build(const float* bvh, int n_nodes, const unsigned char* leaf_cop, Wid
         }
         for (auto it = order.rbegin(); it != order.rend(); ++it) {
             const int y = *it;
-            const double a = area(bn[y]) + 1e-30;
-            if (bn[y].leaf) {
-                for (int k = 1; k <= 4; k++) F[y][k] = a * kCostLeaf;
-                continue;
-            }
+            if (bn[y].leaf) continue;
             const int l = bn[y].left, r = bn[y].right;
             double best = 1e300;                  // y as a record: its own best cut below
             for (int k1 = 1; k1 <= 3; k1++) best = std::min(best, F[l][k1] + F[r][4 - k1]);
-            const double own = a * kCostRec + best;   // = a * C(y)
-            F[y][1] = own;
+            F[y][1] = (area(bn[y]) + 1e-30) * kCostRec + best;
             for (int k = 2; k <= 4; k++) {
                 F[y][k] = F[y][k - 1];
                 split[y][k] = split[y][k - 1];
-                if (k == 2 && own <= F[y][k]) split[y][k] = 0;
                 for (int k1 = 1; k1 < k; k1++) {
                     const double c = F[l][k1] + F[r][k - k1];
                     if (c < F[y][k]) { F[y][k] = c; split[y][k] = (signed char)k1; }
@@ -161,50 +146,32 @@ int wide_build(const float* bvh, int n_nodes, const unsigned char* leaf_cop, Wid
             }
         }
     }
-    // expands subtree y into at most k members (PT_WIDE_COLLAPSE 1), in preorder
+    // expands subtree y into at most k members, in preorder
     std::function<void(int, int, int*, int&)> expand = [&](int y, int k, int* f, int& n) {
         const int k1 = bn[y].leaf ? 0 : split[y][k];
         if (k1 == 0) { f[n++] = y; return; }
         expand(bn[y].left, k1, f, n);
         expand(bn[y].right, k - k1, f, n);
     };
-    // record frontiers: [left, right], then the internal member of largest surface area
-    // replaced by its two children (in place: the list stays in preorder) until 4 members
+    // a record's frontier: the best cut of its two children's subtrees (in preorder)
     auto frontier = [&](int x, int* f) {
         if (bn[x].leaf) { f[0] = x; return 1; }   // a root leaf: a record with that one child
-        if (kWideCollapse == 1) {
-            const int l = bn[x].left, r = bn[x].right;
-            int bk = 1;
-            double best = 1e300;
-            for (int k1 = 1; k1 <= 3; k1++)
-                if (F[l][k1] + F[r][4 - k1] < best) { best = F[l][k1] + F[r][4 - k1]; bk = k1; }
-            int n = 0;
-            expand(l, bk, f, n);
-            expand(r, 4 - bk, f, n);
-            return n;
-        }
-        int n = 2;
-        f[0] = bn[x].left;
-        f[1] = bn[x].right;
-        while (n < 4) {
-            int best = -1;
-            double ba = -1.0;
-            for (int k = 0; k < n; k++)
-                if (!bn[f[k]].leaf && area(bn[f[k]]) > ba) { ba = area(bn[f[k]]); best = k; }
-            if (best < 0) break;
-            const int y = f[best];
-            for (int k = n; k > best + 1; k--) f[k] = f[k - 1];
-            f[best] = bn[y].left;
-            f[best + 1] = bn[y].right;
-            n++;
-        }
+        const int l = bn[x].left, r = bn[x].right;
+        int bk = 1;
+        double best = 1e300;
+        for (int k1 = 1; k1 <= 3; k1++)
+            if (F[l][k1] + F[r][4 - k1] < best) { best = F[l][k1] + F[r][4 - k1]; bk = k1; }
+        int n = 0;
+        expand(l, bk, f, n);
+        expand(r, 4 - bk, f, n);
         return n;
     };
-    // numbering: a record's children take consecutive indices (cbase + j).  Groups are
-    // allocated breadth-first until kTopBreadth indices (the records the kernel may stage in
-    // LDS come first), then -- PT_WIDE_ORDER 1 -- each remaining subtree is numbered depth-first
-    // (its groups contiguous), or -- 2 -- breadth-first inside the subtree, or -- 0 -- the
-    // breadth-first order continues over the whole tree.
+    // numbering: a record's children take consecutive indices (cbase + j).  Best-first: the
+    // pending record of largest box area (the likeliest to be visited by an incoherent ray)
+    // has its group allocated next, so the first indices -- the ones the kernel stages in LDS
+    // -- hold the most visited records.  (Measured against breadth-first numbering: +0.3% on
+    // the C3 / C4 stand-ins, 13% fewer global-memory record visits in the CPU model; numbering
+    // each subtree below the LDS top depth-first or breadth-first inside it: within 0.3%.)
     out.g_of.assign(n_nodes, -1);
     std::vector<int> recs{0}, rdepth{0};          // binary node of each record, in discovery order
     std::vector<int> parent_g{-1}, parent_slot{0};
@@ -238,11 +205,7 @@ int wide_build(const float* bvh, int n_nodes, const unsigned char* leaf_cop, Wid
         kids[ri] = k;
         nkids[ri] = n;
     };
-    size_t qi = 0;
-    if (kWideOrder == 3) {
-        // best-first: the pending record of largest box area (the likeliest to be visited by
-        // an incoherent ray) has its group allocated next, so the first indices -- the ones
-        // the kernel stages in LDS -- hold the most visited records
+    {
         std::vector<std::pair<double, int>> heap{{area(bn[recs[0]]), 0}};
         std::vector<int> found;
         while (!heap.empty() && !overflow) {
@@ -254,26 +217,6 @@ int wide_build(const float* bvh, int n_nodes, const unsigned char* leaf_cop, Wid
             for (int c : found) {
                 heap.emplace_back(area(bn[recs[c]]), c);
                 std::push_heap(heap.begin(), heap.end());
-            }
-        }
-        qi = recs.size();
-    }
-    for (; qi < recs.size() && (kWideOrder == 0 || next < kTopBreadth) && !overflow; qi++) process(qi, nullptr);
-    const size_t pending = recs.size();
-    for (size_t r0 = qi; r0 < pending && !overflow; r0++) {   // the subtrees below the breadth-first top
-        std::vector<int> work{(int)r0}, found;
-        for (size_t w = 0; w < work.size() && !overflow;) {
-            int ri;
-            if (kWideOrder == 1) { ri = work.back(); work.pop_back(); }   // depth-first
-            else ri = work[w++];                                          // breadth-first in the subtree
-            found.clear();
-            process((size_t)ri, &found);
-            if (kWideOrder == 1) {
-                for (auto it = found.rbegin(); it != found.rend(); ++it) work.push_back(*it);
-                if (work.empty()) break;
-                w = 0;
-            } else {
-                work.insert(work.end(), found.begin(), found.end());
             }
         }
     }
@@ -327,9 +270,6 @@ int wide_build(const float* bvh, int n_nodes, const unsigned char* leaf_cop, Wid
             float* b = &out.lbox[(size_t)out.g_of[c] * 8];
             b[0] = bn[c].lo[0]; b[1] = bn[c].hi[0]; b[2] = bn[c].lo[1]; b[3] = bn[c].hi[1];
             b[4] = bn[c].lo[2]; b[5] = bn[c].hi[2];
-            // ... and in the leaf's own (otherwise unused) record slot: the leaf phase's exact
-            // re-test reads it there, beside its siblings
-            std::memcpy(&out.rec[(size_t)out.g_of[c] * 16], b, 8 * sizeof(float));
             out.n_leaves++;
         }
     }

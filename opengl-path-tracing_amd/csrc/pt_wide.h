@@ -46,6 +46,13 @@
 namespace ptw {
 
 constexpr int kRecQuads = 4;          // float4 per record (64 B)
+// pending-child stack entries per lane (measured, same-process A/B on the C3 / C4 stand-ins:
+// 4 entries +0.4% / +0.2% over 3 with the optimal collapse and best-first numbering; 3 was
+// +0.5% / +2.6% over 2 in round 4)
+#ifndef PT_WIDE_STACK
+#define PT_WIDE_STACK 4
+#endif
+constexpr int kStack = PT_WIDE_STACK;
 constexpr int kMaxRecords = 1 << 24;  // cbase << 8 in a 32-bit stack entry
 
 // Per-ray constants of the conservative child test: rd = RN(1/d) and the addends ord -+ E

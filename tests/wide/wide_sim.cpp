@@ -131,7 +131,7 @@ WideOut wide_walk(f3 o, f3 d, float t0) {
     const ptw::WRay wr = ptw::make_wray(o, rd, W.cw, std::signbit(d.x), std::signbit(d.y), std::signbit(d.z));
     int cur = 0, R = -1;
 #ifndef STACK_K
-#define STACK_K 2
+#define STACK_K ptw::kStack   // the kernel's depth (pt_wide.h)
 #endif
     uint32_t e[STACK_K] = {};
     long last_line = -1;
