@@ -12,7 +12,11 @@ round)
   SKIP_TESTS=1 PMC_WORLDS=${PMC_WORLDS:-8} bash tools/gpu_round.sh ;;
 configs)
   bash tools/gpu_configs.sh || exit $?
-  bash tools/gpu_interactive.sh ;;
+  bash tools/gpu_interactive.sh || exit $?
+  # render blocks per CU of the overlapped one-frame launches (tuning key 18), render only
+  timeout -k 10 300 python tools/interactive_fps.py --rows none --frames 400 \
+      --combos "${IFPS_COMBOS:-9=0;18=2;18=3;18=4;18=6}" > "$O/${ROUND_TAG}_ifps_key18.json" 2>&1
+  echo "key18 rc=$?"; cat "$O/${ROUND_TAG}_ifps_key18.json" ;;
 checks)
   timeout -k 10 900 python -u -m pytest tests -x -q -m gpu --timeout 400 --timeout-method thread > "$O/${ROUND_TAG}_gpu_tests.log" 2>&1; rc=$?
   tail -3 "$O/${ROUND_TAG}_gpu_tests.log"; [ $rc -eq 0 ] || exit $rc
