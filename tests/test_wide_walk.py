@@ -111,3 +111,16 @@ def test_leaf_certificate_fuzz(tmp_path, seed):
     assert r.returncode == 0 and out["violations"] == 0, r.stderr[:2000]
     assert out["exact_fail"] > 1000                   # the sample does reach the failing cases
     assert out["certified"] > 0.8 * out["hits"] and out["flat_certified"] > 0.7 * out["flat_hits"]
+
+
+def test_select_transition_matches_rules(tmp_path):
+    """The walk's select-only transition (ptw::wide_visit / wide_pop) against its rules written
+    out as branches (tests/wide/visit_equiv.cpp): pushes, flushes of a full stack, resumed
+    records, pops down to the resume position, stack depths 2, 3 and 4."""
+    exe = str(tmp_path / "visit_equiv")
+    subprocess.check_call(["g++", "-O2", "-std=c++17", "-march=x86-64-v3", "-o", exe,
+                           os.path.join(REPO, "tests", "wide", "visit_equiv.cpp")])
+    r = subprocess.run([exe, "400000", "7"], capture_output=True, text=True)
+    out = json.loads(r.stdout.strip().splitlines()[-1])
+    assert r.returncode == 0 and out["mismatches"] == 0, r.stderr[:2000]
+    assert out["flushes"] > 10000 and out["empty_pops"] > 10000 and out["pushes"] > 100000
