@@ -2492,9 +2492,15 @@ static int enqueue_render(pt_ctx* c, int frame_first, int n_frames, int acc_firs
         // previous render find free slots beside the next render instead of waiting for its
         // blocks to retire.  1080p Cornell, one frame per dispatch (tools/interactive_fps.py):
         // 0.534 -> 0.514 ms per frame, and 0.68 -> 0.55-0.58 with every frame shown
-        // (pt_present, lag 2); accumulate pass 243 -> 103 us.
+        // (pt_present, lag 2); accumulate pass 243 -> 103 us.  Round 5, 3 slots, 600-800 frames
+        // (profiles/ab/r05i_interactive_sweep.json, r05j_*): render only, 2 / 3 / 4 / 5 blocks
+        // per CU 0.513 / 0.473 / 0.537 / 0.493 ms per frame; every frame presented at lag 2, 3
+        // blocks 0.55-0.62 against 0.530 at 5.  So 3 slots take 3 blocks per CU, or 5 when the
+        // caller presented after the previous render (aces_fuse).
         if (overlap && nt == 256) {
-            const int bpc = c->overlap_bpc ? c->overlap_bpc : std::max(1, mw - (c->overlap_slots >= 3 ? 2 : 1));
+            const int bpc = c->overlap_bpc ? c->overlap_bpc
+                          : c->overlap_slots >= 3 ? (c->aces_fuse ? std::max(1, mw - 2) : 3)
+                                                  : std::max(1, mw - 1);
             grid.x = std::min<unsigned>(grid.x, (unsigned)(bpc * c->n_cu));
         }
         // global scene: the top nodes staged per block, at most what mw blocks per CU fit in
