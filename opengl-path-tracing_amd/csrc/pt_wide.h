@@ -189,8 +189,7 @@ PT_HD int wide_next(int cur, uint32_t pend, int cbase, uint32_t (&e)[K], int& R)
     const bool more = (rest & 0xffu) != 0u;
     // a push onto a full stack flushes it: the walk resumes this record at the next slot
     const bool flush = fresh & more & (e[K - 1] != 0u);
-    const bool put = more & !flush;                     // rest becomes the top
-    const bool down = fresh & put;                      // push: the others move down
+    const bool down = fresh & more;                     // push: the others move down
     const bool up = !fresh & !more & (p != 0u);         // popped the top's last child
     uint32_t n[K];
 #if defined(__HIP_DEVICE_COMPILE__)
@@ -198,11 +197,9 @@ PT_HD int wide_next(int cur, uint32_t pend, int cbase, uint32_t (&e)[K], int& R)
 #endif
     for (int k = 0; k < K; k++) {
         const uint32_t below = k + 1 < K ? e[k + 1 < K ? k + 1 : k] : 0u;
-        const uint32_t above = k > 0 ? e[k > 0 ? k - 1 : 0] : rest;
-        uint32_t v = up ? below : e[k];
-        v = down ? above : v;
-        if (k == 0) v = put ? rest : v;
-        n[k] = flush ? 0u : v;
+        const uint32_t v = up ? below : e[k];
+        n[k] = k == 0 ? (more ? rest : v)                // rest becomes the top
+                      : (down ? e[k > 0 ? k - 1 : 0] : v);
     }
 #if defined(__HIP_DEVICE_COMPILE__)
 #pragma unroll
@@ -210,7 +207,22 @@ PT_HD int wide_next(int cur, uint32_t pend, int cbase, uint32_t (&e)[K], int& R)
     for (int k = 0; k < K; k++) e[k] = n[k];
     const int pos = ty == 1u ? child << 3 : -2 - ((child << 1) | (int)(ty == 3u));
     const int r = R;
-    R = flush ? ((cur & ~7) | ((j2 >> 1) + 1)) : (p ? R : -1);
+    R = p ? R : -1;
+    // the flush, rare, off the common path: a wave-uniform branch around its four selects
+    // (+0.45% / +0.49% on the C3 / C4 stand-ins over selecting every step)
+#if defined(__HIP_DEVICE_COMPILE__)
+    if (__any(flush)) {
+#else
+    {
+#endif
+        if (flush) {
+#if defined(__HIP_DEVICE_COMPILE__)
+#pragma unroll
+#endif
+            for (int k = 0; k < K; k++) e[k] = 0u;
+            R = (cur & ~7) | ((j2 >> 1) + 1);
+        }
+    }
     return p ? pos : r;
 }
 

@@ -44,11 +44,26 @@
 #define A_PERM(x) asm volatile("v_perm_b32 %0, %1, %0, %2" : "+v"(x) : "v"(w), "v"(0x05040100u));
 #define A_CND(x) asm volatile("v_cndmask_b32 %0, %0, %1, %2" : "+v"(x) : "v"(b), "s"(m));
 #define A_CMP(x) asm volatile("v_cmp_le_f32 %0, %1, %2" : "=s"(m) : "v"(x), "v"(b));
+#define A_XOR(x) asm volatile("v_xor_b32 %0, %1, %0" : "+v"(x) : "v"(w));
+#define A_SHL(x) asm volatile("v_lshlrev_b32 %0, 3, %0" : "+v"(x));
+#define A_BITOP3(x) asm volatile("v_bitop3_b32 %0, %1, %0, %2 bitop3:0xca" : "+v"(x) : "v"(w), "v"(b));
+#define A_ANDOR(x) asm volatile("v_and_or_b32 %0, %1, %0, %2" : "+v"(x) : "v"(w), "v"(b));
+#define A_OR3(x) asm volatile("v_or3_b32 %0, %1, %0, %2" : "+v"(x) : "v"(w), "v"(b));
+#define A_MAXI(x) asm volatile("v_max_i32 %0, %1, %0" : "+v"(x) : "v"(w));
+#define A_SUBU(x) asm volatile("v_sub_u32 %0, %1, %0" : "+v"(x) : "v"(w));
+#define A_FFBL(x) asm volatile("v_ffbl_b32 %0, %0" : "+v"(x));
+#define A_CNDV(x) asm volatile("v_cndmask_b32 %0, %0, %1, vcc" : "+v"(x) : "v"(b));
+#define A_PAIRV(x) asm volatile("v_cmp_le_f32 vcc, %0, %1\n\ts_nop 1\n\tv_cndmask_b32 %0, %0, %2, vcc" : "+v"(x) : "v"(b), "v"(c) : "vcc");
+#define A_PAIRS(x) { unsigned long long q_; asm volatile("v_cmp_le_f32 %1, %0, %2\n\ts_nop 1\n\tv_cndmask_b32 %0, %0, %3, %1" : "+v"(x), "=&s"(q_) : "v"(b), "v"(c)); }
+#define A_CNDVW(x) asm volatile("v_cndmask_b32 %0, %0, %1, vcc" : "+v"(x) : "v"(b));
 #define A_MOV(x) asm volatile("v_mov_b32 %0, %1" : "=v"(x) : "v"(b)); asm volatile("" :: "v"(x));
 FORM(fma, A_FMA, 0) FORM(fmac, A_FMAC, 0) FORM(add, A_ADD, 0) FORM(mul, A_MUL, 0) FORM(min, A_MIN, 0)
 FORM(max3, A_MAX3, 0) FORM(med3, A_MED3, 0) FORM(pkfma, A_PKFMA, 0) FORM(mix, A_MIX, 0) FORM(cvtub, A_CVTUB, 0)
 FORM(cvtu32, A_CVTU32, 0) FORM(ldexp, A_LDEXP, 0) FORM(and, A_AND, 0) FORM(addu, A_ADDU, 0) FORM(bfe, A_BFE, 0)
 FORM(perm, A_PERM, 0) FORM(cnd, A_CND, 0) FORM(cmp, A_CMP, 0) FORM(mov, A_MOV, 0)
+FORM(xor_, A_XOR, 0) FORM(shl, A_SHL, 0) FORM(bitop3, A_BITOP3, 0) FORM(andor, A_ANDOR, 0) FORM(or3, A_OR3, 0)
+FORM(pairv, A_PAIRV, 0) FORM(pairs, A_PAIRS, 0)
+FORM(maxi, A_MAXI, 0) FORM(subu, A_SUBU, 0) FORM(ffbl, A_FFBL, 0) FORM(cndv, A_CNDV, 0)
 typedef void (*KF)(float*, unsigned long long*, float);
 int main() {
     const int ncu = 256;
@@ -58,7 +73,10 @@ int main() {
         {"v_fma_mix_f32", k_mix<0>}, {"v_cvt_f32_ubyte1", k_cvtub<0>}, {"v_cvt_f32_u32", k_cvtu32<0>},
         {"v_ldexp_f32", k_ldexp<0>}, {"v_and_b32", k_and<0>}, {"v_add_u32", k_addu<0>}, {"v_bfe_u32", k_bfe<0>},
         {"v_perm_b32", k_perm<0>}, {"v_cndmask_b32 (sgpr mask)", k_cnd<0>}, {"v_cmp_le_f32 (sgpr dst)", k_cmp<0>},
-        {"v_mov_b32", k_mov<0>}};
+        {"v_mov_b32", k_mov<0>}, {"v_xor_b32", k_xor_<0>}, {"v_lshlrev_b32", k_shl<0>}, {"v_bitop3_b32", k_bitop3<0>},
+        {"v_and_or_b32", k_andor<0>}, {"v_or3_b32", k_or3<0>}, {"v_max_i32", k_maxi<0>}, {"v_sub_u32", k_subu<0>},
+        {"v_ffbl_b32", k_ffbl<0>}, {"v_cndmask_b32 (vcc)", k_cndv<0>},
+        {"v_cmp vcc + s_nop 1 + v_cndmask vcc (pair)", k_pairv<0>}, {"v_cmp sgpr + s_nop 1 + v_cndmask sgpr (pair)", k_pairs<0>}};
     float* out; unsigned long long* cyc;
     if (hipMalloc(&out, (size_t)ncu * 1024 * 4) != hipSuccess || hipMalloc(&cyc, (size_t)ncu * 16 * 8) != hipSuccess) return 1;
     hipEvent_t e0, e1;
