@@ -1114,7 +1114,9 @@ __global__ __launch_bounds__(NT, MINW) void k_render_sm(KParams p) {
                         float half_b = pt::dot(oc, d);
                         float cq = pt::dot(oc, oc) - s0.w;
                         float disc = half_b * half_b - a * cq;
-                        float ht = disc < 0.0f ? -1.0f : pt::div_g(-half_b - pt::sqrt_g(disc), a);
+                        // the IEEE division sequence, not div_g: its range guard's four compares
+                        // cost more than the sequence (same quotient; +0.6% on C2, round 5)
+                        float ht = disc < 0.0f ? -1.0f : (-half_b - pt::sqrt_g(disc)) / a;
                         if (COUNT) c.sph++;
                         if ((ht > 0.0001f) & (ht < t)) {
                             t = ht;

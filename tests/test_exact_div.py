@@ -156,7 +156,8 @@ int main(int argc, char** argv) {
 
 
 def test_guarded_division_is_correctly_rounded(tmp_path):
-    """pt_math.h div_g (the sphere root's division in the state-machine kernel): the exact
+    """pt_math.h div_g (the guarded quotient; the kernel's sphere root uses the IEEE sequence
+    since round 5, DESIGN.md §6, and the camera ray div_mk under a static guard): the exact
     reciprocal + Markstein correction over its guard (both magnitudes in [2^-60, 2^60]),
     2e7 random pairs incl. exact multiples, near ties and all-ones divisor mantissas."""
     src = tmp_path / "dg.c"
