@@ -140,7 +140,55 @@ PT_HD f3 operator/(f3 a, float s) { return mk(a.x / s, a.y / s, a.z / s); }
 PT_HD float dot(f3 a, f3 b) { return (a.x * b.x + a.y * b.y) + a.z * b.z; }
 PT_HD f3 cross(f3 a, f3 b) { return mk(a.y * b.z - b.y * a.z, a.z * b.x - b.z * a.x, a.x * b.y - b.x * a.y); }
 // The guard of rcp_fast / sqrt_fast; NaN fails it.
-PT_HD bool fast_range(float q) { return q >= 0x1p-100f && q <= 0x1p100f; }
+// Range predicates of the guards and hit windows, in two forms that agree on every input:
+// float compares (_f) and one unsigned compare of the bit patterns (_u; positive floats order
+// as their bits, and zeros, negatives, inf and NaN fall outside each window as they fail the
+// float compares).  tests/test_int_windows.py checks the agreement on special values and
+// random bit patterns; PT_INT_GUARDS / PT_INT_WINDOWS pick the _u forms in the kernel.
+PT_HD bool range_abs_f(float v, float lo, float hi) {      // |v| in [lo, hi], 0 < lo <= hi
+    const float a = __builtin_fabsf(v);
+    return (a >= lo) & (a <= hi);
+}
+PT_HD bool range_abs_u(float v, float lo, float hi) {
+    return (fbits(v) & 0x7fffffffu) - fbits(lo) <= fbits(hi) - fbits(lo);
+}
+PT_HD bool guard_f(float v, float lo, float hi) { return (v == 0.0f) | range_abs_f(v, lo, hi); }
+PT_HD bool guard_u(float v, float lo, float hi) { return ((fbits(v) & 0x7fffffffu) == 0u) | range_abs_u(v, lo, hi); }
+// 1e-4 < x < t and 1e-4 <= x < t, for t > 1e-4 (t starts at +inf and only takes accepted
+// distances, which exceed 1e-4)
+PT_HD bool win_open_f(float x, float t) { return (x > 0.0001f) & (x < t); }
+PT_HD bool win_open_u(float x, float t) {
+    const uint32_t lo = fbits(0.0001f) + 1u;
+    return fbits(x) - lo < fbits(t) - lo;
+}
+PT_HD bool win_closed_f(float x, float t) { return (x >= 0.0001f) & (x < t); }
+PT_HD bool win_closed_u(float x, float t) {
+    const uint32_t lo = fbits(0.0001f);
+    return fbits(x) - lo < fbits(t) - lo;
+}
+PT_HD bool fast_range_f(float q) { return q >= 0x1p-100f && q <= 0x1p100f; }
+PT_HD bool fast_range_u(float q) { return fbits(q) - fbits(0x1p-100f) <= fbits(0x1p100f) - fbits(0x1p-100f); }
+#if defined(PT_INT_GUARDS)
+PT_HD bool in_range_abs(float v, float lo, float hi) { return range_abs_u(v, lo, hi); }
+PT_HD bool in_guard(float v, float lo, float hi) { return guard_u(v, lo, hi); }
+#else
+PT_HD bool in_range_abs(float v, float lo, float hi) { return range_abs_f(v, lo, hi); }
+PT_HD bool in_guard(float v, float lo, float hi) { return guard_f(v, lo, hi); }
+#endif
+#if defined(PT_INT_WINDOWS)
+PT_HD bool win_open(float x, float t) { return win_open_u(x, t); }
+PT_HD bool win_closed(float x, float t) { return win_closed_u(x, t); }
+#else
+PT_HD bool win_open(float x, float t) { return win_open_f(x, t); }
+PT_HD bool win_closed(float x, float t) { return win_closed_f(x, t); }
+#endif
+PT_HD bool fast_range(float q) {
+#if defined(PT_INT_GUARDS)
+    return fast_range_u(q);
+#else
+    return fast_range_f(q);
+#endif
+}
 PT_HD float sqrt_g(float q) {
     if (fast_range(q)) return sqrt_fast(q);
     return fsqrt(q);

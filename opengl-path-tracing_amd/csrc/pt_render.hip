@@ -313,14 +313,13 @@ __device__ __forceinline__ float qdiv(float a, float b, float rb) {
     return __builtin_fmaf(r, rb, q);
 }
 
-__device__ __forceinline__ bool in_guard(float v, float lo, float hi) {
-    float a = __builtin_fabsf(v);
-    return (v == 0.0f) | ((a >= lo) & (a <= hi));
-}
-__device__ __forceinline__ bool in_range_abs(float v, float lo, float hi) {
-    float a = __builtin_fabsf(v);
-    return (a >= lo) & (a <= hi);
-}
+// in_guard / in_range_abs: pt_math.h (float compares, or one unsigned window with
+// PT_INT_GUARDS)
+using pt::in_guard;
+using pt::in_range_abs;
+
+using pt::win_open;     // the hit windows 1e-4 < x < t and 1e-4 <= x < t (pt_math.h)
+using pt::win_closed;
 
 // The box tests' "tn <= tf && tn <= t" is evaluated as tn <= min(tf, t):
 // one compare instead of two plus a scalar AND of their lane masks, which sat on the walk
@@ -463,8 +462,8 @@ __device__ __forceinline__ void leaf_pair_tests(const SceneView& S, bool at, int
     }
     tb = cop ? ta : tb;
     const f3 na3 = mk(nda.x, nda.y, nda.z), nb3 = mk(ndb.x, ndb.y, ndb.z);
-    const bool na = at & (ta > 0.0001f) & (ta < t);
-    const bool nb = at & (tb >= 0.0001f) & (tb < t);
+    const bool na = at & win_open(ta, t);
+    const bool nb = at & win_closed(tb, t);
     const unsigned long long ma = __ballot(na), mb = __ballot(nb);
     const int ca = __popcll(ma), n = ca + __popcll(mb);
     bool oka = false, okb = false;
@@ -1118,7 +1117,7 @@ __global__ __launch_bounds__(NT, MINW) void k_render_sm(KParams p) {
                         // cost more than the sequence (same quotient; +0.6% on C2, round 5)
                         float ht = disc < 0.0f ? -1.0f : (-half_b - pt::sqrt_g(disc)) / a;
                         if (COUNT) c.sph++;
-                        if ((ht > 0.0001f) & (ht < t)) {
+                        if (win_open(ht, t)) {
                             t = ht;
                             hprim = -2 - si;
                         }
@@ -1176,8 +1175,8 @@ __global__ __launch_bounds__(NT, MINW) void k_render_sm(KParams p) {
             }
             bool c1 = false, c2 = false;
             if (at) {
-                c1 = (h1 > 0.0001f) & (h1 < t) & ((h1 < h2) | (h2 < 0.0001f));
-                c2 = !c1 & (h2 > 0.0001f) & (h2 < t);
+                c1 = win_open(h1, t) & ((h1 < h2) | (h2 < 0.0001f));
+                c2 = !c1 & win_open(h2, t);
             }
             if (LDS && !COUNT && p.cons_walk) {
                 // the culling walk stopped here on the conservative test: the reference tests
