@@ -313,8 +313,7 @@ __device__ __forceinline__ float qdiv(float a, float b, float rb) {
     return __builtin_fmaf(r, rb, q);
 }
 
-// in_guard / in_range_abs: pt_math.h (float compares, or one unsigned window with
-// PT_INT_GUARDS)
+// in_guard / in_range_abs: pt_math.h (one unsigned window on the bit patterns)
 using pt::in_guard;
 using pt::in_range_abs;
 

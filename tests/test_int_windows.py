@@ -1,8 +1,8 @@
 """The unsigned-window forms of the walk guard, the normalize range test and the hit windows
 (pt_math.h range_abs_u / guard_u / fast_range_u / win_open_u / win_closed_u) agree with their
 float-compare forms on every input class: zeros, window edges and their neighbours, inf, NaN
-and denormals of both signs, and random bit patterns (tests/math/int_windows.cpp).  The kernel
-may use either form (PT_INT_GUARDS / PT_INT_WINDOWS) with the same image."""
+and denormals of both signs, and random bit patterns (tests/math/int_windows.cpp).  The kernel's
+guards use the unsigned forms; its hit windows may (PT_INT_WINDOWS), with the same image."""
 import json
 import os
 import subprocess
