@@ -119,8 +119,10 @@ def roofline_from(pmc, stale, lib_sha, avg_launch_ms, n_launch, segments_per_lau
               (a wave64 VALU instruction holds a SIMD-32 for 2 cycles)
       texture achieved = TD_TD_BUSY cycles per launch (summed over CUs) / live launch time;
               peak = 256 CUs x clock (the texture-data unit that returns every vector-memory
-              load; the global-memory walk's scattered gathers keep it busy)
-    `bound` is the one with the larger fraction.  HBM stays a secondary field: the scene is
+              load; the global-memory walk's scattered gathers keep it busy).  Busy includes
+              cycles stalled on L1 (TD_TC_STALL): `stall_frac` and `unstalled_frac` say how much
+    `bound` is the one with the larger fraction, the texture unit ranked by its unstalled
+    fraction (its busy figure is mostly stall on the global walk).  HBM stays a secondary field: the scene is
     LDS / L2 / MALL-resident, and the algorithmic bytes are mostly LDS and
     L1 reads.  Occupancy: resident waves per SIMD (SQ_WAVE_CYCLES is counted in quad-cycles on
     gfx950) against the 8 wave slots."""
@@ -134,33 +136,42 @@ def roofline_from(pmc, stale, lib_sha, avg_launch_ms, n_launch, segments_per_lau
         r["pmc_stale"] = stale
     if pmc is not None:
         c = pmc["counters_per_launch"]
-        clk = pmc["clock_ghz"]
+        clk = pmc.get("clock_ghz")     # None when no pass recorded GRBM_GUI_ACTIVE: no peaks
         cands = {}
-        if c.get("SQ_INSTS_VALU"):
+        if c.get("SQ_INSTS_VALU") and clk:
             a = c["SQ_INSTS_VALU"] / t / 1e9
             cands["valu"] = {"achieved": round(a, 2), "peak": round(N_SIMD * clk / 2.0, 2), "unit": "G wave-VALU instr/s",
                              "per_segment": round(c["SQ_INSTS_VALU"] / segments_per_launch, 2)}
-        if c.get("TD_TD_BUSY_sum"):
+        if c.get("TD_TD_BUSY_sum") and clk:
             a = c["TD_TD_BUSY_sum"] / t / 1e9
             cands["texture"] = {"achieved": round(a, 2), "peak": round(N_CU * clk, 2), "unit": "G TD-busy cycles/s",
                                 "per_segment": round(c["TD_TD_BUSY_sum"] / segments_per_launch, 2)}
         for k, v in cands.items():
             v["frac"] = round(v["achieved"] / v["peak"], 4)
+        # TD busy cycles include the cycles the unit sits stalled on L1 (TD_TC_STALL): only the
+        # rest is data-return work, and that unstalled share is what the bound is chosen on
+        rank_frac = {k: v["frac"] for k, v in cands.items()}
+        if "texture" in cands and c.get("TD_TC_STALL_sum"):
+            stall = c["TD_TC_STALL_sum"] / c["TD_TD_BUSY_sum"]
+            cands["texture"]["stall_frac"] = round(stall, 4)
+            cands["texture"]["unstalled_frac"] = round(cands["texture"]["frac"] * (1.0 - stall), 4)
+            rank_frac["texture"] = cands["texture"]["unstalled_frac"]
         if cands:
-            b = max(cands, key=lambda k: cands[k]["frac"])
+            b = max(cands, key=lambda k: rank_frac[k])
             r.update(bound=b, achieved=cands[b]["achieved"], peak=cands[b]["peak"], unit=cands[b]["unit"],
                      frac=cands[b]["frac"])
             r["bounds"] = cands
-        r["clock_ghz_pmc"] = round(clk, 3)
+        r["clock_ghz_pmc"] = round(clk, 3) if clk else None
         if c.get("SQ_WAVE_CYCLES") and c.get("GRBM_GUI_ACTIVE"):
             w = 4.0 * c["SQ_WAVE_CYCLES"] / (c["GRBM_GUI_ACTIVE"] / 8.0 * N_SIMD)
             r["occupancy"] = {"waves_per_simd": round(w, 2), "peak": WAVES_PER_SIMD_PEAK,
                               "frac": round(w / WAVES_PER_SIMD_PEAK, 4)}
-        if c.get("SQ_ACTIVE_INST_VALU"):
+        if c.get("SQ_ACTIVE_INST_VALU") and c.get("SQ_THREAD_CYCLES_VALU"):
             r["active_lanes_per_valu"] = round(c["SQ_THREAD_CYCLES_VALU"] / c["SQ_ACTIVE_INST_VALU"], 2)
         mem = {}
         if c.get("TCP_TOTAL_CACHE_ACCESSES_sum"):
             mem["l1_accesses_per_segment"] = round(c["TCP_TOTAL_CACHE_ACCESSES_sum"] / segments_per_launch, 2)
+        if c.get("TCP_TCC_READ_REQ_sum"):
             mem["l1_to_l2_per_segment"] = round(c["TCP_TCC_READ_REQ_sum"] / segments_per_launch, 2)
         if c.get("SQ_INSTS_VMEM_RD"):
             mem["vmem_load_instr_per_segment"] = round(c["SQ_INSTS_VMEM_RD"] / segments_per_launch, 3)
@@ -188,12 +199,47 @@ def roofline_from(pmc, stale, lib_sha, avg_launch_ms, n_launch, segments_per_lau
     return r
 
 
+def parity_pixels_for(spp, requested):
+    """Pixels of the timed image checked against the oracle: about 4 M oracle pixel-frames
+    (C2: 4096 pixels x 1024 frames, about a second on a 16-CPU share), 512..4096."""
+    if requested is not None:
+        return max(0, int(requested))
+    return int(min(4096, max(512, (1 << 22) // max(spp, 1))))
+
+
+def check_timed_image(img, sb, W, H, spp, bounces, row0, stride, n_pix, seed, threads):
+    """Parity of the image the timed steps left in the accumulator: every step renders frames
+    1..spp with accumulate = 0 on frame 1 (computeShader.c:505-554, :548-551), so the image is
+    that of spp reference dispatches.  n_pix pixels drawn (seeded) from the rows this image
+    holds (global row y = row0 + k * stride for local row k) are rendered by the CPU oracle
+    (test infrastructure, after the timed region) and compared word for word."""
+    import numpy as np
+    sys.path.insert(0, os.path.join(REPO, "tests"))
+    import oracle_lib
+    rows = img.shape[0]
+    rng = np.random.default_rng(seed)
+    n_pix = min(n_pix, rows * W)
+    flat = rng.choice(rows * W, size=n_pix, replace=False)
+    ky, xs = flat // W, flat % W
+    ys = row0 + ky * stride
+    t0 = time.perf_counter()
+    want = oracle_lib.render_pixels(sb, W, H, xs, ys, max_bounce=bounces, n_frames=spp, threads=threads)
+    dt = time.perf_counter() - t0
+    got = np.ascontiguousarray(img[ky, xs], np.float32)
+    mism = int(np.count_nonzero(got.view(np.uint32) != want.view(np.uint32)))
+    return {"kind": "timed image, sampled pixels vs CPU oracle", "frames": "1..%d" % spp, "pixels": int(n_pix),
+            "words": int(4 * n_pix), "mismatches": mism, "seed": int(seed), "oracle_s": round(dt, 2)}
+
+
 def measure(cfg, args, ctx, steps, warmup, cold=True, W=None, H=None, spp=None, bounces=None, chunk=None,
-            dump=False):
+            dump=False, parity_pixels=0, full_frames=0):
     """One configuration on this rank: scene (rank 0 builds it, N > 1 broadcasts), optional
     cold first render, `warmup` untimed steps, `steps` timed steps (barrier + synchronize on
     both sides, max over ranks), an untimed counting pass over the same frames, and the
-    roofline from the PMC summary of this build and per-rank workload."""
+    roofline from the PMC summary of this build and per-rank workload.  After the timed
+    region, rank 0 checks `parity_pixels` sampled pixels of the timed image against the CPU
+    oracle, and with `full_frames` re-renders frames 1..full_frames on the same context for a
+    full-frame comparison with the cpu_baseline leg's oracle image."""
     import torch
     import pt_host
     import pt_scenes
@@ -302,6 +348,18 @@ def measure(cfg, args, ctx, steps, warmup, cold=True, W=None, H=None, spp=None, 
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
 
+    # the image the timed steps produced (N > 1: the assembled frame; otherwise this
+    # context's rows, y = rank + k * world), kept for the parity check and --dump-frame
+    timed_img = None
+    if rank == 0 and (parity_pixels or dump):
+        timed_img = img.cpu().numpy() if img is not None else pt.read_rgba32f()
+    parity = None
+    if rank == 0 and parity_pixels and steps > 0:
+        full = img is not None
+        parity = check_timed_image(timed_img, sb, W, H, spp, bounces, 0 if full else pt.row0,
+                                   1 if full else pt.row_stride, parity_pixels,
+                                   0x5EED + sum(map(ord, cfg)), cpu_share()[0])
+
     # untimed counting pass over the same frames: exact reference-semantics work counts
     pt.set_counting(True)
     tot = dict(segments=0, node_visits=0, tri_tests=0, sphere_tests=0, hits=0)
@@ -325,9 +383,13 @@ def measure(cfg, args, ctx, steps, warmup, cold=True, W=None, H=None, spp=None, 
     pmc, stale, lib_sha = pmc_for(pmc_json, pt_host.LIB_PATH, W, H, chunk, scene, world)
     roofline = roofline_from(pmc, stale, lib_sha, avg_launch_ms, n_launch, seg_rank / len(launches),
                              alg_bytes / len(launches))
-    frame = None
-    if dump and rank == 0:
-        frame = img.cpu().numpy() if img is not None else pt.read_rgba32f()
+    frame = timed_img if dump else None
+    full_img = None
+    if full_frames and rank == 0 and world == 1:
+        # frames 1..full_frames on the timed context (its tuning, learned tile order and
+        # scratch), for the word-for-word comparison with the cpu_baseline leg's oracle image
+        pt.render(1, full_frames, 0)
+        full_img = pt.read_rgba32f()
     rows_local = pt.rows_local
     pt.close()
     ms_per_step = dt / steps * 1e3
@@ -335,7 +397,7 @@ def measure(cfg, args, ctx, steps, warmup, cold=True, W=None, H=None, spp=None, 
         "cfg": cfg, "scene": scene, "W": W, "H": H, "spp": spp, "bounces": bounces, "chunk": chunk,
         "use_graph": use_graph, "value": seg_all * steps / dt / 1e6, "ms_per_step": ms_per_step,
         "ms_per_frame": ms_per_step / spp, "cold_ms": cold_ms, "segments": seg_all, "roofline": roofline,
-        "sb": sb, "frame": frame, "rows_local": rows_local,
+        "sb": sb, "frame": frame, "rows_local": rows_local, "parity": parity, "full_img": full_img,
     }
 
 
@@ -371,6 +433,12 @@ def main():
     ap.add_argument("--traffic-json", default=None,
                     help="PMC summary for the headline config (default profiles/pmc/<config>[_wN].json, "
                          "tools/pmc_traffic.py)")
+    ap.add_argument("--parity-pixels", type=int, default=None,
+                    help="pixels of each timed image checked against the CPU oracle after the timed region "
+                         "(default: about 4 M oracle pixel-frames, 512..4096; 0 = skip)")
+    ap.add_argument("--force-dist", action="store_true",
+                    help="take the N>1 path (process group, scene broadcast, device row copy, all-gather) "
+                         "even at world size 1: a one-GPU rehearsal of the RCCL leg")
     args = ap.parse_args()
 
     import torch
@@ -378,12 +446,23 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    distributed = world > 1
+    distributed = world > 1 or args.force_dist
+    if distributed and args.share_of > 1:
+        raise SystemExit("--share-of is a one-process proxy; do not combine it with torch.distributed.run")
+    if distributed and world == 1:
+        # a world-1 process group launched without torch.distributed.run: a loopback rendezvous
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        if "MASTER_PORT" not in os.environ:
+            import socket
+            s = socket.socket()
+            s.bind(("127.0.0.1", 0))
+            os.environ["MASTER_PORT"] = str(s.getsockname()[1])
+            s.close()
+        os.environ.setdefault("RANK", "0")
+        os.environ.setdefault("WORLD_SIZE", "1")
     ndev = max(1, torch.cuda.device_count())
     device = local_rank % ndev
     if args.share_of > 1:
-        if distributed:
-            raise SystemExit("--share-of is a one-process proxy; do not combine it with torch.distributed.run")
         world = args.share_of
     ctx = dict(world=world, rank=rank, device=device, distributed=distributed)
     if distributed:
@@ -394,9 +473,14 @@ def main():
         else:
             dist.init_process_group("gloo")
         ctx["dist"] = dist
+        ctx["backend"] = dist.get_backend()
 
+    spp_head = args.spp or CONFIGS[args.config][3]
+    want_cpu = rank == 0 and world == 1 and not args.no_cpu_baseline
     m = measure(args.config, args, ctx, args.steps, args.warmup, cold=not args.no_cold, W=args.width,
-                H=args.height, spp=args.spp, bounces=args.bounces, chunk=args.chunk, dump=bool(args.dump_frame))
+                H=args.height, spp=args.spp, bounces=args.bounces, chunk=args.chunk, dump=bool(args.dump_frame),
+                parity_pixels=parity_pixels_for(spp_head, args.parity_pixels),
+                full_frames=args.cpu_spp if want_cpu and args.parity_pixels != 0 else 0)
     W, H, spp, bounces, scene = m["W"], m["H"], m["spp"], m["bounces"], m["scene"]
 
     sec_cfgs = []
@@ -407,25 +491,35 @@ def main():
         sec_cfgs = [c for c in args.secondary.split(",") if c]
     secondary = []
     for c in sec_cfgs:
-        s = measure(c, args, ctx, args.secondary_steps, 1, cold=False)
+        s = measure(c, args, ctx, args.secondary_steps, 1, cold=False,
+                    parity_pixels=parity_pixels_for(CONFIGS[c][3], args.parity_pixels))
         secondary.append({
             "config": c, "workload": "%s: %s %dx%d, %d spp in launches of %d frames, %d bounces" % (
                 c, s["scene"], s["W"], s["H"], s["spp"], s["chunk"], s["bounces"]),
             "value": round(s["value"], 3), "unit": "Mrays/s", "steps": args.secondary_steps, "warmup": 1,
             "ms_per_step": round(s["ms_per_step"], 3), "ms_per_frame": round(s["ms_per_frame"], 4),
-            "segments_per_step": int(s["segments"]), "roofline": s["roofline"]})
+            "segments_per_step": int(s["segments"]), "roofline": s["roofline"], "parity": s["parity"]})
 
     cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+    full_parity = None
+    if want_cpu:
+        import numpy as np
         sys.path.insert(0, os.path.join(REPO, "tests"))
         import oracle_lib
         threads, share = cpu_share()
         if args.cpu_threads:
             threads = args.cpu_threads
         t1 = time.perf_counter()
-        _, ccnt = oracle_lib.render(m["sb"], W, H, max_bounce=bounces, n_frames=args.cpu_spp, threads=threads,
-                                    counters=True)
+        cimg, ccnt = oracle_lib.render(m["sb"], W, H, max_bounce=bounces, n_frames=args.cpu_spp, threads=threads,
+                                       counters=True)
         cdt = time.perf_counter() - t1
+        if m["full_img"] is not None:
+            # the oracle image of the timed baseline sample, word for word against the GPU's
+            # frames 1..cpu_spp on the timed context
+            g = np.ascontiguousarray(m["full_img"], np.float32)
+            full_parity = {"kind": "full frame vs the cpu_baseline leg's oracle image", "frames": "1..%d" % args.cpu_spp,
+                           "pixels": int(W * H), "words": int(g.size),
+                           "mismatches": int(np.count_nonzero(g.view(np.uint32) != cimg.view(np.uint32)))}
         cpu = {"value": round(float(ccnt[0]) / cdt / 1e6, 3), "unit": "Mrays/s", "cores": threads, "kind": "port",
                "cpu_model": cpu_model(), "host_cpus": os.cpu_count(), "cpu_share": share,
                "sample": "CPU restatement of computeShader.c semantics (oracle/pt_oracle.cpp, -O3, %d threads = this "
@@ -455,8 +549,17 @@ def main():
             "segments_per_step": int(m["segments"]),
             "roofline": m["roofline"],
             "cpu_baseline": cpu,
+            "parity": None,
             "secondary": secondary,
         }
+        checks = [p for p in (m["parity"], full_parity) if p]
+        if checks:
+            line["parity"] = {"words": sum(p["words"] for p in checks),
+                              "mismatches": sum(p["mismatches"] for p in checks),
+                              "checks": checks, "oracle": "oracle/pt_oracle.cpp (CPU restatement, test infrastructure)"}
+        if distributed:
+            line["config"]["process_group"] = {"backend": ctx["backend"], "world": world,
+                                               "rehearsal": bool(args.force_dist and world == 1)}
         if world > 1:
             line["roofline"]["share"] = "rank 0's share: rows y = 0 mod %d, %d rows" % (world, m["rows_local"])
         if args.share_of > 1:   # a proxy line: this GPU's rate on rank 0's share, n_gpus stays 1

@@ -183,6 +183,15 @@ int pt_set_kernel(pt_ctx* ctx, int variant);
  *         tree threaded in preorder whose internal boxes contain their children's, the
  *         LDS-staged walk tests nodes with a cheaper conservative slab test and re-tests a
  *         leaf's box exactly before one of its triangles may move t.
+ * key 16 = wide global-memory walk (0 = automatic, 1 = off: the binary walk).  Scenes too
+ *         large for LDS with a nested tree walk a 4-wide tree of quantised child boxes
+ *         (DESIGN.md §5.10).
+ * key 17 = threads per workgroup of the wide walk: 256, 512, 768 or 1024 (0 = automatic, 256).
+ * key 18 = overlapped short renders: 256-thread blocks per CU, 1..8 (0 = automatic: 3 with
+ *         three or more render slots, 5 when the caller presents every frame).
+ * key 19 = leaf re-test certificate (0 = automatic, 1 = off).  The wide walk skips the exact
+ *         leaf-box re-test for a hit whose triangle data proves it passes;
+ *         only for uploaded trees whose leaf boxes contain their triangles' vertices.
  * None of these change the image (each pixel's frames stay in order in one lane). */
 int pt_set_tuning(pt_ctx* ctx, int key, int value);
 

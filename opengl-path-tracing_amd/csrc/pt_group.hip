@@ -366,14 +366,16 @@ int pt_group_present_begin(pt_group* g, int buf) {
     if (buf < 0 || buf >= kGroupPresentBufs) return gfail(g, PT_E_ARG, "present buffer must be 0..3");
     const long long n = (long long)g->W * (long long)g->H;
     GHIP(g, hipSetDevice(g->devs[0]));
-    if (!g->present_dev[buf]) {
+    // each resource on its own null check: an earlier call that failed part-way (say the
+    // pinned allocation after the device one) must not leave later calls recording on null events
+    if (!g->present_dev[buf])
         GHIP(g, hipMalloc(&g->present_dev[buf], std::max<long long>(n, 1) * sizeof(uchar4)));
+    if (!g->present_host[buf])
         GHIP(g, hipHostMalloc((void**)&g->present_host[buf], std::max<long long>(n, 1) * sizeof(uchar4),
                               hipHostMallocDefault));
-        GHIP(g, hipEventCreateWithFlags(&g->ev_copied[buf], hipEventDisableTiming));
-        GHIP(g, hipEventCreate(&g->ev_g0[buf]));
-        GHIP(g, hipEventCreate(&g->ev_g1[buf]));
-    }
+    if (!g->ev_copied[buf]) GHIP(g, hipEventCreateWithFlags(&g->ev_copied[buf], hipEventDisableTiming));
+    if (!g->ev_g0[buf]) GHIP(g, hipEventCreate(&g->ev_g0[buf]));
+    if (!g->ev_g1[buf]) GHIP(g, hipEventCreate(&g->ev_g1[buf]));
     // a buffer begun again before its end: its previous copy must land first
     if (g->present_pending[buf]) GHIP(g, hipEventSynchronize(g->ev_copied[buf]));
     g->present_pending[buf] = false;

@@ -127,3 +127,49 @@ def test_bench_roofline_per_rank_share_and_bounds(tmp_path):
     assert r["active_lanes_per_valu"] == 40.0 and r["memory_pipe"]["l2_hit_rate"] == 0.9
     none = bench.roofline_from(None, "no PMC pass", sha, t_ms, 1, 1e9, 1e12)
     assert none["frac"] is None and none["pmc_stale"] == "no PMC pass"
+
+
+def test_bench_texture_bound_ranked_unstalled():
+    """The texture unit's busy figure includes cycles stalled on L1 (TD_TC_STALL): the line
+    reports stall_frac and unstalled_frac, and the bound is chosen on the unstalled share, so
+    a walk whose TD is 95% busy but 61% stalled reports its VALU bound instead."""
+    import bench
+    clk, t_ms = 2.4, 100.0
+    cyc = clk * 1e9 * t_ms * 1e-3
+    ctr = {"SQ_INSTS_VALU": 0.73 * 512 * cyc, "TD_TD_BUSY_sum": 0.95 * 256 * cyc,
+           "TD_TC_STALL_sum": 0.61 * 0.95 * 256 * cyc}
+    r = bench.roofline_from({"counters_per_launch": ctr, "clock_ghz": clk}, None, "0" * 64, t_ms, 1, 1e9, 1e12)
+    tx = r["bounds"]["texture"]
+    assert abs(tx["stall_frac"] - 0.61) < 1e-3 and abs(tx["unstalled_frac"] - 0.95 * 0.39) < 1e-3
+    assert r["bound"] == "valu" and abs(r["frac"] - 0.73) < 1e-3
+
+
+def test_bench_roofline_partial_counters():
+    """A PMC summary holding only some counter groups (a hand-made or partial one) must not
+    stop the line: fields whose counters are missing are left out."""
+    import bench
+    ctr = {"SQ_INSTS_VALU": 1e9, "SQ_ACTIVE_INST_VALU": 1e8, "TCP_TOTAL_CACHE_ACCESSES_sum": 5e9}
+    r = bench.roofline_from({"counters_per_launch": ctr, "clock_ghz": 2.4}, None, "0" * 64, 100.0, 1, 1e9, 1e12)
+    assert r["bound"] == "valu" and "active_lanes_per_valu" not in r
+    assert r["memory_pipe"] == {"l1_accesses_per_segment": 5.0}
+
+
+def test_bench_timed_image_parity_check(cornell_scene):
+    """bench.check_timed_image: sampled pixels of a timed image against the oracle, for a full
+    frame and for a row-split share (global row y = row0 + k * stride); one flipped bit in a
+    sampled pixel is one mismatching word."""
+    import numpy as np
+    import bench
+    import oracle_lib as O
+    W, Hh, spp = 40, 24, 3
+    img = O.render(cornell_scene, W, Hh, max_bounce=4, n_frames=spp)
+    r = bench.check_timed_image(img, cornell_scene, W, Hh, spp, 4, 0, 1, 200, 7, 4)
+    assert r["pixels"] == 200 and r["words"] == 800 and r["mismatches"] == 0 and r["frames"] == "1..3"
+    share = img[1::3]                                   # rank 1 of 3
+    assert bench.check_timed_image(share, cornell_scene, W, Hh, spp, 4, 1, 3, 100, 7, 4)["mismatches"] == 0
+    bad = img.copy()
+    bad.view(np.uint32)[...] ^= 1                       # every word off by one ulp
+    r = bench.check_timed_image(bad, cornell_scene, W, Hh, spp, 4, 0, 1, 50, 7, 4)
+    assert r["mismatches"] == 200
+    assert bench.parity_pixels_for(1024, None) == 4096 and bench.parity_pixels_for(4096, None) == 1024
+    assert bench.parity_pixels_for(256, 0) == 0

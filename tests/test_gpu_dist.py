@@ -95,3 +95,38 @@ def test_bench_share_proxy_line(tmp_path):
     want = pt.read_rgba32f()
     pt.close()
     assert_bitwise(img, want[0::4], "share proxy rows vs one context")
+
+
+@pytest.mark.parametrize("config", ["C2", "C4"])
+def test_bench_rccl_leg_world_one(tmp_path, cornell_scene, config):
+    """The RCCL leg of bench.py rehearsed on one GPU (--force-dist at world 1): the nccl
+    process group with device_id, pt_dist.broadcast_scene on cuda tensors, pt_copy_rows_device
+    into a cuda send buffer and all_gather_into_tensor -- the calls the driver's 8-GPU run
+    makes.  The line names RCCL's backend, its timed-image parity check against the oracle
+    passes, and the dumped frame equals one context's render bit for bit."""
+    import json
+    W, Hh, spp, chunk = 160, 90, 6, 3
+    out = str(tmp_path / "frame.npy")
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0", MASTER_ADDR="127.0.0.1")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "1",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), "bench.py", "--gpus", "1",
+           "--config", config, "--dist-backend", "nccl", "--force-dist", "--width", str(W), "--height", str(Hh),
+           "--spp", str(spp), "--chunk", str(chunk), "--steps", "2", "--warmup", "1", "--no-cold",
+           "--no-cpu-baseline", "--parity-pixels", "300", "--dump-frame", out]
+    r = subprocess.run(cmd, cwd=REPO, env=env, capture_output=True, text=True, timeout=420)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
+    line = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
+    pg = line["config"]["process_group"]
+    assert pg["backend"] == "nccl" and pg["world"] == 1 and pg["rehearsal"] is True, pg
+    assert line["parity"]["mismatches"] == 0 and line["parity"]["words"] == 1200, line["parity"]
+    assert line["value"] > 0
+    img = np.load(out)
+    import pt_scenes
+    sc = cornell_scene if config == "C2" else H.setupBuffers(*pt_scenes.write_scene("sponza", os.path.join(REPO, "scenes")))
+    pt = H.PathTracer(W, Hh, max_bounce=8)
+    pt.upload(sc)
+    pt.render(1, spp, 0)
+    want = pt.read_rgba32f()
+    pt.close()
+    assert img.shape == want.shape
+    assert_bitwise(img, want, "RCCL world-1 bench frame vs one context")

@@ -65,6 +65,8 @@ def reduce(pmc, meta):
             for cn, v in ctr.items():
                 per[cn].append(v)
             per["launch_ms_" + name].append(sum(ms.values()))
+            if "GRBM_GUI_ACTIVE" in ctr:       # this pass's own clock (its counters, its launch time)
+                per["clock_ghz_" + name].append(ctr["GRBM_GUI_ACTIVE"] / 8.0 / (sum(ms.values()) * 1e6))
             for kind, v in ms.items():
                 per["%s_ms_%s" % (kind, name)].append(v)
     avg = {k: sum(v) / len(v) for k, v in per.items()}
@@ -79,11 +81,17 @@ def reduce(pmc, meta):
         out["fetch_bytes_raw"] = avg["FETCH_SIZE"] * 1024
         out["write_bytes"] = avg["WRITE_SIZE"] * 1024
         out["hbm_bytes_per_launch"] = 2 * avg["FETCH_SIZE"] * 1024 + avg["WRITE_SIZE"] * 1024
-    if "GRBM_GUI_ACTIVE" in avg:
-        # GRBM_GUI_ACTIVE sums the 8 XCDs' busy clocks; the clock is held over the launch
-        cycles = avg["GRBM_GUI_ACTIVE"] / 8.0
-        pass_ms = [avg[k] for k in ("launch_ms_sq2", "launch_ms_mem", "launch_ms_l2") if k in avg]
-        out["clock_ghz"] = cycles / (pass_ms[0] * 1e6)
+    # GRBM_GUI_ACTIVE sums the 8 XCDs' busy clocks; each pass that records it gives its own
+    # clock (its cycles over its own launch time), and the passes' clocks are averaged
+    clocks = [v for k, v in avg.items() if k.startswith("clock_ghz_")]
+    if "GRBM_GUI_ACTIVE" in avg and not clocks:
+        print("pmc_traffic: GRBM_GUI_ACTIVE without a launch time; no clock", file=sys.stderr)
+    elif "GRBM_GUI_ACTIVE" not in avg:
+        print("pmc_traffic: no pass recorded GRBM_GUI_ACTIVE; no clock, no busy fractions", file=sys.stderr)
+    if clocks:
+        out["clock_ghz"] = sum(clocks) / len(clocks)
+        # cycles of one average launch at that clock
+        cycles = out["clock_ghz"] * 1e6 * out.get("pmc_launch_ms", 0.0)
         if "SQ_INSTS_VALU" in avg:
             # a wave64 VALU op holds a SIMD-32 for 2 cycles (MI355X_MICROARCH.md); 1024 SIMDs
             out["valu_busy_frac"] = 2.0 * avg["SQ_INSTS_VALU"] / (1024.0 * cycles)
