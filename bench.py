@@ -200,11 +200,11 @@ def roofline_from(pmc, stale, lib_sha, avg_launch_ms, n_launch, segments_per_lau
 
 
 def parity_pixels_for(spp, requested):
-    """Pixels of the timed image checked against the oracle: about 4 M oracle pixel-frames
-    (C2: 4096 pixels x 1024 frames, about a second on a 16-CPU share), 512..4096."""
+    """Pixels of the timed image checked against the oracle: about 16 M oracle pixel-frames
+    (C2: 16384 pixels x 1024 frames, about 1.5 s on a 16-CPU share), 1024..16384."""
     if requested is not None:
         return max(0, int(requested))
-    return int(min(4096, max(512, (1 << 22) // max(spp, 1))))
+    return int(min(16384, max(1024, (1 << 24) // max(spp, 1))))
 
 
 def check_timed_image(img, sb, W, H, spp, bounces, row0, stride, n_pix, seed, threads):

@@ -171,5 +171,5 @@ def test_bench_timed_image_parity_check(cornell_scene):
     bad.view(np.uint32)[...] ^= 1                       # every word off by one ulp
     r = bench.check_timed_image(bad, cornell_scene, W, Hh, spp, 4, 0, 1, 50, 7, 4)
     assert r["mismatches"] == 200
-    assert bench.parity_pixels_for(1024, None) == 4096 and bench.parity_pixels_for(4096, None) == 1024
+    assert bench.parity_pixels_for(1024, None) == 16384 and bench.parity_pixels_for(4096, None) == 4096
     assert bench.parity_pixels_for(256, 0) == 0
