@@ -1333,6 +1333,12 @@ __device__ __forceinline__ uchar4 aces_px(float4 v) {
 #define PT_ACCUM_PIX 4
 #endif
 constexpr int kAccumPix = PT_ACCUM_PIX;
+// Long launches (more than kShortLaunch frames): 2 pixels per thread and 8 frames per load
+// group (same-process A/B, a 1080p/8 share's 1024-frame launch: +1.6% for the whole render
+// against one frame per group, +1.1% with 4 x 4; the full 1080p image unchanged).  Short
+// launches keep 4 pixels and one frame per group (the pass beside the next one-frame render).
+constexpr int kAccumPixLong = 2, kAccumFramesLong = 8;
+template <int kAccumPix, int kAccumFrames>
 __global__ __launch_bounds__(256) void k_accum_frames(KParams p) {
     resolve_frames(p);
     // the render that used these queue heads has ended (this pass runs after it): ready them
@@ -1355,7 +1361,24 @@ __global__ __launch_bounds__(256) void k_accum_frames(KParams p) {
         }
         acc[j] = (on[j] && p.acc_first) ? p.accum[idx[j]] : make_float4(0, 0, 0, 0);
     }
-    for (int k = 0; k < p.n_frames; k++) {
+    // frames in groups of kAccumFrames whose loads are issued together, then applied in frame
+    // order: one load group in flight per thread made a long launch's pass latency-bound when
+    // few pixels give few threads (a 1080p/8 share's 1024 frames: 0.96 ms for 3.2 GB)
+    int k = 0;
+    for (; k + kAccumFrames <= p.n_frames; k += kAccumFrames) {
+        f3 v[kAccumFrames][kAccumPix];
+#pragma unroll
+        for (int u = 0; u < kAccumFrames; u++)
+#pragma unroll
+            for (int j = 0; j < kAccumPix; j++)
+                v[u][j] = on[j] ? nt_load3(p.rgb + 3 * ((size_t)(k + u) * (size_t)n + (size_t)idx[j])) : mk(0, 0, 0);
+#pragma unroll
+        for (int u = 0; u < kAccumFrames; u++)
+#pragma unroll
+            for (int j = 0; j < kAccumPix; j++)
+                acc[j] = accumulate(acc[j], v[u][j], p.frame_first + k + u, k + u > 0 || p.acc_first == 1);
+    }
+    for (; k < p.n_frames; k++) {
         f3 v[kAccumPix];
 #pragma unroll
         for (int j = 0; j < kAccumPix; j++)
@@ -2172,14 +2195,23 @@ static bool lds_staged(const pt_ctx* c) {
     return PT_LDS_WIDE && !c->counting && !c->minw && c->cfg.rays_per_pixel == 1 && c->lds_bytes <= kLdsSceneMax;
 }
 
+// Round 6: the frames per item follow the frames each resident lane renders in the launch,
+// F = pixels * frames / resident lanes.  An item costs a fixed pull and set-up o plus g frames
+// of c each, and a launch ends in a tail of about half an item, so the time per lane is about
+// F c + (F / g) o + g c / 2: least at g = sqrt(2 F o / c).  Fitted to same-process A/Bs of C2's
+// 1024-frame launch (profiles/ab/r06f_*): a 1080p/8 share (F = 578) is fastest at 9-12 frames
+// per item (+1.4% over 16), a 1080p/4 share (F = 1157) at 12, the whole image (F = 4628) at
+// 16 or more; global-memory scenes cost about 5x more per frame (c), so about sqrt(5) fewer.
+// The caps: C2 16 +0.5% over 8; C3 stand-in 4 +8% over 8.
 static int plan_group(const pt_ctx* c, int n_frames) {
     if (c->group_force > 0) return std::min(c->group_force, n_frames);
-    const int waves = c->minw ? c->minw : 6;
+    const int waves = c->minw ? c->minw : (lds_staged(c) ? 7 : 6);
     const double lanes = (double)c->n_cu * 4.0 * waves * 64.0;
     const double px = (double)c->rows_local * c->cfg.width;
     const bool lds_scene = lds_staged(c);
-    int g = (int)(px * n_frames / (16.0 * lanes));
-    g = std::max(1, std::min(g, lds_scene ? 16 : 4));  // C2: 16 +0.5% over 8; C3 stand-in: 4 +8% over 8
+    const double F = px * n_frames / lanes;
+    int g = (int)(std::sqrt(F) * (lds_scene ? 0.416 : 0.19) + 0.5);
+    g = std::max(1, std::min(g, lds_scene ? 16 : 4));
     return std::min(g, n_frames);
 }
 
@@ -2572,8 +2604,14 @@ static int enqueue_render(pt_ctx* c, int frame_first, int n_frames, int acc_firs
             // a captured graph: its replays are not followed by pt_present_begin's check)
             p.aces_out = (c->aces_fuse && !frame_dev) ? c->rgba8 : nullptr;
             c->stage_ok = p.aces_out != nullptr;
-            hipLaunchKernelGGL(k_accum_frames, dim3((unsigned)((px + 256 * kAccumPix - 1) / (256 * kAccumPix))), dim3(256),
-                               0, c->stream, p);
+            if (n_frames > kShortLaunch)
+                hipLaunchKernelGGL((k_accum_frames<kAccumPixLong, kAccumFramesLong>),
+                                   dim3((unsigned)((px + 256 * kAccumPixLong - 1) / (256 * kAccumPixLong))), dim3(256), 0,
+                                   c->stream, p);
+            else
+                hipLaunchKernelGGL((k_accum_frames<kAccumPix, 1>),
+                                   dim3((unsigned)((px + 256 * kAccumPix - 1) / (256 * kAccumPix))), dim3(256), 0,
+                                   c->stream, p);
             if (overlap) {
                 HIPCHK(c, hipEventRecord(c->ev_adone[re], c->stream));
                 c->adone_rec[re] = true;
