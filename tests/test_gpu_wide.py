@@ -132,3 +132,38 @@ def test_orphan_leaf_node_is_skipped(cornell_scene):
     for variant in (3, 0):
         got = render(sc, W, Hh, 3, variant=variant)
         assert_bitwise(got, want, "orphan leaf, variant %d" % variant)
+
+
+def test_leaf_certificate_gate_and_key19(scenes, cornell_scene):
+    """The leaf re-test certificate stands on every leaf box containing its
+    triangles' vertices (checked at upload).  A nested tree with leaf boxes shrunk so that they
+    exclude part of their triangles still takes the wide walk, but must keep the exact re-test
+    everywhere: the reference tests those leaves against the shrunk boxes, and the image is the
+    oracle's.  And tuning key 19 (certificate off) never changes the image."""
+    for name, sc0, variant, n_shrunk in (("cornell", cornell_scene, 3, 8), ("p", scenes["p"], 0, None)):
+        sc = dict(sc0)
+        nodes = np.array(sc["nodes"], np.float32).reshape(-1, 12)
+        leaves = [i for i in range(len(nodes)) if nodes[i, 8] > -1.0]
+        ext = lambda i: float(np.prod(np.maximum(nodes[i, 4:7] - nodes[i, 0:3], 1e-3)))
+        for i in sorted(leaves, key=ext, reverse=True)[:n_shrunk]:   # the largest (Cornell) or all (p)
+            ax = int(np.argmax(nodes[i, 4:7] - nodes[i, 0:3]))
+            nodes[i, 4 + ax] = np.float32(0.5 * (nodes[i, ax] + nodes[i, 4 + ax]))   # max shrinks to the middle
+        assert H.bvh_culling_ok(nodes)                           # still nested: the wide walk runs
+        sc["nodes"] = nodes
+        W, Hh = 64, 48
+        got = render(sc, W, Hh, 3, variant=variant)
+        want = O.render(sc, W, Hh, max_bounce=8, n_frames=3)
+        assert_bitwise(got, want, "%s: shrunk leaf boxes" % name)
+        assert not np.array_equal(want, O.render(sc0, W, Hh, max_bounce=8, n_frames=3)), \
+            "%s: the shrunk boxes must change the reference's image (else the test tests nothing)" % name
+    sc = scenes["bunny"]
+    W, Hh = 96, 64
+    imgs = []
+    for k19 in (0, 1):
+        pt = H.PathTracer(W, Hh, max_bounce=8)
+        pt.set_key(19, k19)
+        pt.upload(sc)
+        pt.render(1, 4, 0)
+        imgs.append(pt.read_rgba32f())
+        pt.close()
+    assert_bitwise(imgs[0], imgs[1], "key 19 = 0 vs 1")
