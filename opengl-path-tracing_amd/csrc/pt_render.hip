@@ -74,7 +74,8 @@ struct KParams {
     unsigned* reset_work;          // k_accum_frames zeroes these queue heads (an overlap slot's) for its next use
     const int* frame_dev;          // progressive graph: device frame counter (null = use frame_first)
     int frame_offset;              // this launch's frame offset from *frame_dev
-    const unsigned* tile_perm;     // queue order of 8x8 tiles, entries (ty << 16) | tx (null = raster order)
+    const unsigned* tile_perm;     // queue order of the tiles, entries (ty << 16) | tx (null = raster order)
+    int tile_shift;                // tiles of 64 pixels: (8 << tile_shift) columns x (8 >> tile_shift) local rows
     unsigned* tile_cost;           // per-tile segment counts of this launch (null = off)
     // frame-split work items (state-machine kernel): a queue item is (pixel, `group`
     // consecutive frames); with rgb != null the lane stores each frame's pixel colour (12 B)
@@ -841,9 +842,10 @@ __global__ __launch_bounds__(NT, MINW) void k_render_sm(KParams p) {
 #endif
     const f3 cpos = mk(p.cam[0], p.cam[1], p.cam[2]), cfwd = mk(p.cam[3], p.cam[4], p.cam[5]);
     const f3 cright = mk(p.cam[6], p.cam[7], p.cam[8]), cup = mk(p.cam[9], p.cam[10], p.cam[11]);
-    const int tiles_x = (p.W + 7) >> 3;
+    const int tsh = p.tile_shift, tw = 8 << tsh, th = 8 >> tsh;   // tile: tw columns x th local rows
+    const int tiles_x = (p.W + tw - 1) >> (3 + tsh);
     const unsigned n_groups = SPLIT ? (unsigned)((p.n_frames + p.group - 1) / p.group) : 1u;
-    const unsigned total_ids = (unsigned)tiles_x * (unsigned)((p.rows_local + 7) >> 3) * n_groups * 64u;
+    const unsigned total_ids = (unsigned)tiles_x * (unsigned)((p.rows_local + th - 1) >> (3 - tsh)) * n_groups * 64u;
     const int n_nodes = p.sc.n_nodes;
     const bool use_tris = !(p.flags & PT_FLAG_NO_TRIANGLES) && n_nodes > 0;
     // walk start for a ray inside the root box: its first child (the counting build walks
@@ -1046,8 +1048,8 @@ __global__ __launch_bounds__(NT, MINW) void k_render_sm(KParams p) {
                             ty = (int)(tile / (unsigned)tiles_x);
                         }
                         tile = (unsigned)(ty * tiles_x + tx);
-                        int cx = tx * 8 + (int)(w & 7u);
-                        int crow = ty * 8 + (int)(w >> 3);
+                        int cx = tx * tw + (int)(w & (unsigned)(tw - 1));
+                        int crow = ty * th + (int)(w >> (3 + tsh));
                         int cy = p.row0 + crow * p.row_stride;
                         if ((cx < p.W) & (crow < p.rows_local) & (cx < p.x_limit) & (cy < p.y_limit)) {
                             lx = cx;
@@ -1429,6 +1431,9 @@ __global__ __launch_bounds__(256) void k_aces(const float4* __restrict__ src, uc
 // on gfx950; a copy too large for the resident waves' worth of 256-thread workgroups is
 // shared by wider ones (lds_threads), so mid-size scenes keep the LDS walk at 4+ waves per
 // SIMD instead of the global-memory walk.
+#ifndef PT_TILE_AUTO
+#define PT_TILE_AUTO 1
+#endif
 #ifndef PT_LDS_SCENE_MAX_KIB
 #define PT_LDS_SCENE_MAX_KIB 152
 #endif
@@ -1495,6 +1500,7 @@ struct pt_ctx {
     unsigned* d_tile_cost = nullptr;
     unsigned* d_tile_perm = nullptr;
     int n_tiles = 0, tiles_x = 1;
+    int tile_shift = 0, tile_key = 0;   // tile shape (KParams::tile_shift) and tuning key 20 (0 = automatic)
     bool adaptive = true;
     hipGraph_t graph = nullptr;
     hipGraphExec_t graph_exec = nullptr;
@@ -1574,6 +1580,8 @@ static unsigned pack_tile(const pt_ctx* c, unsigned t) {
 
 
 static void drop_graph(pt_ctx* c);   // a captured graph bakes in scene/camera/config
+static int ensure_tiles(pt_ctx* c);  // the tile shape this context's next launch uses
+
 
 static int fail(pt_ctx* c, int code, const std::string& msg) {
     if (c) c->err = msg;
@@ -1585,6 +1593,27 @@ static int fail(pt_ctx* c, int code, const std::string& msg) {
         if (e_ != hipSuccess)                                                               \
             return fail(ctx, PT_E_HIP, std::string(#call ": ") + hipGetErrorString(e_));     \
     } while (0)
+
+// Tile shape of the work queue: 64 pixels as (8 << s) columns x (8 >> s) local rows (tuning
+// key 20; automatic: ensure_tiles).  Recomputes the tile count and resets the queue order.
+static int set_tiles(pt_ctx* c, int s) {
+    c->tile_shift = s;
+    const int tw = 8 << s, th = 8 >> s;
+    c->tiles_x = (c->cfg.width + tw - 1) / tw;
+    c->n_tiles = c->tiles_x * ((c->rows_local + th - 1) / th);
+    (void)hipFree(c->d_tile_perm);
+    (void)hipFree(c->d_tile_cost);
+    c->d_tile_perm = c->d_tile_cost = nullptr;
+    std::vector<unsigned> ident(std::max(c->n_tiles, 1));
+    for (size_t i = 0; i < ident.size(); i++) ident[i] = pack_tile(c, (unsigned)i);
+    HIPCHK(c, hipMalloc(&c->d_tile_perm, ident.size() * sizeof(unsigned)));
+    HIPCHK(c, hipMalloc(&c->d_tile_cost, ident.size() * sizeof(unsigned)));
+    HIPCHK(c, hipMemcpy(c->d_tile_perm, ident.data(), ident.size() * sizeof(unsigned), hipMemcpyHostToDevice));
+    HIPCHK(c, hipMemset(c->d_tile_cost, 0, ident.size() * sizeof(unsigned)));
+    c->order_sorted = false;
+    c->order_skip = 0;
+    return PT_OK;
+}
 
 static void free_scene(pt_ctx* c) {
     (void)hipFree(c->d_nodes); (void)hipFree(c->d_tris); (void)hipFree(c->d_mats); (void)hipFree(c->d_spheres);
@@ -1644,15 +1673,9 @@ int pt_create(const pt_config* cfg, pt_ctx** out) {
         HIPCHK(c, hipDeviceTotalMem(&total_mem, cfg->device));
         c->scratch_budget = std::min<size_t>(32ull << 30, total_mem / 4);
     }
-    c->n_tiles = ((cfg->width + 7) / 8) * ((c->rows_local + 7) / 8);
-    c->tiles_x = (cfg->width + 7) / 8;
     {
-        std::vector<unsigned> ident(std::max(c->n_tiles, 1));
-        for (size_t i = 0; i < ident.size(); i++) ident[i] = pack_tile(c, (unsigned)i);
-        HIPCHK(c, hipMalloc(&c->d_tile_perm, ident.size() * sizeof(unsigned)));
-        HIPCHK(c, hipMalloc(&c->d_tile_cost, ident.size() * sizeof(unsigned)));
-        HIPCHK(c, hipMemcpy(c->d_tile_perm, ident.data(), ident.size() * sizeof(unsigned), hipMemcpyHostToDevice));
-        HIPCHK(c, hipMemset(c->d_tile_cost, 0, ident.size() * sizeof(unsigned)));
+        int rc = set_tiles(c, 0);   // 8 x 8 until a scene picks the automatic shape (ensure_tiles)
+        if (rc) return rc;
     }
     // default camera (ogl_path_trace.h:53-54)
     const float defcam[12] = {0, -6, 1, 0, 0, 1, 0, 0, 0, 0, 0, 0};
@@ -2118,6 +2141,12 @@ int pt_set_tuning(pt_ctx* c, int key, int value) {
         drop_graph(c);
         return PT_OK;
     }
+    if (key == 20) {
+        if (value < 0 || value > 4) return fail(c, PT_E_ARG, "tile shape: 1..4 = 8x8, 16x4, 32x2, 64x1 (0 = automatic)");
+        c->tile_key = value;
+        HIPCHK(c, hipSetDevice(c->cfg.device));
+        return ensure_tiles(c);
+    }
     if (key == 19) {
         if (value != 0 && value != 1) return fail(c, PT_E_ARG, "leaf re-test certificate: 0 = automatic, 1 = off");
         c->cert_off = value;
@@ -2203,6 +2232,22 @@ static bool lds_staged(const pt_ctx* c) {
 // per item (+1.4% over 16), a 1080p/4 share (F = 1157) at 12, the whole image (F = 4628) at
 // 16 or more; global-memory scenes cost about 5x more per frame (c), so about sqrt(5) fewer.
 // The caps: C2 16 +0.5% over 8; C3 stand-in 4 +8% over 8.
+// The work queue's tile shape (set_tiles): tuning key 20, or automatically 16 x 4 for scenes
+// staged in LDS and 8 x 8 for the global-memory walk.  Same-process A/B (profiles/ab/r06k_*,
+// r06l_*): C2 +0.4% (16 x 4) / +0.4% (32 x 2) over 8 x 8, C5's 4K +0.6% / +0.5%, its 1080p/2,
+// /4, /8 shares +0.1 to +0.2%; the C3 stand-in +0.05%, C4 -0.3% (8 x 8 kept there), C4's 1080p/8
+// share -0.2% / -1.2%.  A shape change drains the context's streams and drops a captured graph
+// (which holds the tile arrays).
+static int ensure_tiles(pt_ctx* c) {
+    const int want = c->tile_key ? c->tile_key - 1 : ((PT_TILE_AUTO && c->scene_ok && lds_staged(c)) ? 1 : 0);
+    if (want == c->tile_shift) return PT_OK;
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    for (int i = 0; i < kMaxSlots; i++)
+        if (c->rstream[i]) HIPCHK(c, hipStreamSynchronize(c->rstream[i]));
+    drop_graph(c);
+    return set_tiles(c, want);
+}
+
 static int plan_group(const pt_ctx* c, int n_frames) {
     if (c->group_force > 0) return std::min(c->group_force, n_frames);
     const int waves = c->minw ? c->minw : (lds_staged(c) ? 7 : 6);
@@ -2476,6 +2521,7 @@ static int enqueue_render(pt_ctx* c, int frame_first, int n_frames, int acc_firs
         p.rgb = c->d_rgb;
     }
     p.tile_perm = c->d_tile_perm;
+    p.tile_shift = c->tile_shift;
     p.tile_cost = (c->adaptive && !c->counting) ? c->d_tile_cost : nullptr;
     if (c->rows_local == 0) return PT_OK;
     // variants: 0 state machine (default), 3 = 0 with the scene forced to stay in global memory
@@ -2505,7 +2551,7 @@ static int enqueue_render(pt_ctx* c, int frame_first, int n_frames, int acc_firs
         // persistent grid: enough resident waves to fill every SIMD; surplus blocks find the
         // queue empty and exit.  Never more blocks than 8x8 tiles (64 lanes per tile).
         size_t lds = use_lds ? (p.cons_walk ? c->lds_bytes_sk : c->lds_bytes) : 0;
-        unsigned tiles = (unsigned)(((p.W + 7) / 8) * ((c->rows_local + 7) / 8));
+        unsigned tiles = (unsigned)c->n_tiles;
         unsigned items = tiles * (unsigned)((n_frames + p.group - 1) / p.group);   // 64-lane items
         // the wide walk's workgroup: wider ones share one LDS copy of more top records
         // (tuning key 17); raysPerPixel > 1 keeps 256 threads
@@ -2692,6 +2738,10 @@ int pt_render_async(pt_ctx* c, int frame_first, int n_frames, int acc_first) {
     if (!c->scene_ok) return fail(c, PT_E_STATE, "pt_render before pt_upload_scene");
     if (n_frames <= 0) return fail(c, PT_E_ARG, "n_frames must be > 0");
     HIPCHK(c, hipSetDevice(c->cfg.device));
+    {
+        int rc0 = ensure_tiles(c);
+        if (rc0) return rc0;
+    }
     if (c->counting) HIPCHK(c, hipMemsetAsync(c->d_counters, 0, 16 * sizeof(unsigned long long), c->stream));
     hipEvent_t ev[2];
     int rc = take_events(c, ev);
@@ -2731,6 +2781,10 @@ int pt_progressive_setup(pt_ctx* c, int frames_per_launch, int launches_per_repl
     HIPCHK(c, hipSetDevice(c->cfg.device));
     HIPCHK(c, hipStreamSynchronize(c->stream));
     drop_graph(c);
+    {
+        int rc0 = ensure_tiles(c);
+        if (rc0) return rc0;
+    }
     if (!c->d_frame) HIPCHK(c, hipMalloc(&c->d_frame, 64));
     {   // no allocation inside the capture: the scratch of the largest sub-launch first
         const int n = launch_frames(c, frames_per_launch);

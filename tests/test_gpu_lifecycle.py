@@ -313,3 +313,30 @@ def test_read_rgba8_fused_view(cornell_scene):
         assert np.array_equal(pt.present_end(f % 2), want), f
         assert np.array_equal(pt.read_rgba8(), want), f
     pt.close()
+
+
+@pytest.mark.parametrize("world", [1, 3, 8])
+def test_tile_shapes_bitwise(cornell_scene, world):
+    """Tuning key 20: the work queue's 64-pixel tiles as 8x8, 16x4, 32x2 or 64x1 (local rows of
+    a row-split rank).  The tile shape changes only which lanes render which pixels together:
+    every shape, switched between renders of one context (with a learned tile order, a captured
+    graph and overlapped short launches), gives the oracle's image for every rank."""
+    W, Hh = 100, 44                       # partial tiles on both edges for every shape
+    want = O.render(cornell_scene, W, Hh, max_bounce=6, n_frames=5)
+    for rank in range(world):
+        pt = H.PathTracer(W, Hh, max_bounce=6, rank=rank, world=world)
+        pt.upload(cornell_scene)
+        for key in (4, 1, 3, 2, 0):
+            pt.set_key(20, key)
+            pt.render(1, 3, 0)
+            pt.render_async(4, 1, 1)
+            pt.render_async(5, 1, 1)
+            assert_bitwise(pt.read_rgba32f(), want[rank::world], "world %d rank %d key 20 = %d" % (world, rank, key))
+        pt.progressive_setup(frames_per_launch=1, launches_per_replay=5)
+        pt.set_key(20, 3)                 # drops the graph; the next setup uses the new shape
+        pt.progressive_setup(frames_per_launch=1, launches_per_replay=5)
+        pt.progressive_run(replays=1)
+        assert_bitwise(pt.read_rgba32f(), want[rank::world], "world %d rank %d graph" % (world, rank))
+        with pytest.raises(H.PTError):
+            pt.set_key(20, 5)
+        pt.close()
