@@ -193,8 +193,8 @@ int pt_set_kernel(pt_ctx* ctx, int variant);
  *         leaf-box re-test for a hit whose triangle data proves it passes;
  *         only for uploaded trees whose leaf boxes contain their triangles' vertices.
  * key 20 = work-queue tile shape: 1 = 8x8, 2 = 16x4, 3 = 32x2, 4 = 64x1 pixels (columns x local
- *         rows), 0 = automatic (16x4 for scenes staged in LDS, 8x8 for the global-memory walk;
- *         DESIGN.md §5.4).  A change drains the context's streams and drops a captured graph.
+ *         rows), 0 = automatic (8x8).  A change drains the context's streams and
+ *         drops a captured graph.
  * None of these change the image (each pixel's frames stay in order in one lane). */
 int pt_set_tuning(pt_ctx* ctx, int key, int value);
 

@@ -1432,7 +1432,7 @@ __global__ __launch_bounds__(256) void k_aces(const float4* __restrict__ src, uc
 // shared by wider ones (lds_threads), so mid-size scenes keep the LDS walk at 4+ waves per
 // SIMD instead of the global-memory walk.
 #ifndef PT_TILE_AUTO
-#define PT_TILE_AUTO 1
+#define PT_TILE_AUTO 0      // 1: 16 x 4 tiles for LDS scenes (measured equal to 8 x 8, ensure_tiles)
 #endif
 #ifndef PT_LDS_SCENE_MAX_KIB
 #define PT_LDS_SCENE_MAX_KIB 152
@@ -2232,12 +2232,11 @@ static bool lds_staged(const pt_ctx* c) {
 // per item (+1.4% over 16), a 1080p/4 share (F = 1157) at 12, the whole image (F = 4628) at
 // 16 or more; global-memory scenes cost about 5x more per frame (c), so about sqrt(5) fewer.
 // The caps: C2 16 +0.5% over 8; C3 stand-in 4 +8% over 8.
-// The work queue's tile shape (set_tiles): tuning key 20, or automatically 16 x 4 for scenes
-// staged in LDS and 8 x 8 for the global-memory walk.  Same-process A/B (profiles/ab/r06k_*,
-// r06l_*): C2 +0.4% (16 x 4) / +0.4% (32 x 2) over 8 x 8, C5's 4K +0.6% / +0.5%, its 1080p/2,
-// /4, /8 shares +0.1 to +0.2%; the C3 stand-in +0.05%, C4 -0.3% (8 x 8 kept there), C4's 1080p/8
-// share -0.2% / -1.2%.  A shape change drains the context's streams and drops a captured graph
-// (which holds the tile arrays).
+// The work queue's tile shape (set_tiles): tuning key 20, else 8 x 8 (with PT_TILE_AUTO, 16 x 4
+// for scenes staged in LDS).  Measured with the builds in alternating order (ABBA, profiles/ab/
+// r06n_*): 16 x 4 and 8 x 8 equal within 0.1% on C2 and C5; the +0.4..0.6% of the first A/Bs
+// (r06k_*, r06l_*, r06m_*) was tools/ab_inproc.py's first-position bias.  A shape change drains
+// the context's streams and drops a captured graph (which holds the tile arrays).
 static int ensure_tiles(pt_ctx* c) {
     const int want = c->tile_key ? c->tile_key - 1 : ((PT_TILE_AUTO && c->scene_ok && lds_staged(c)) ? 1 : 0);
     if (want == c->tile_shift) return PT_OK;

@@ -6,6 +6,9 @@ python tools/ab_inproc.py --libs base,cur --rounds 4 --spp 128 --chunk 128 [--sc
 ('cur' = build/libptrace.so, other names = build/libptrace_<name>.so from tools/ab_build.sh;
  an entry name:k=v[:k=v] adds pt_set_tuning keys for that entry only, e.g. --libs cur,p37:3=8)
 
+The build order rotates every round (each build is timed first equally often): a fixed order
+favoured the later entries by about 0.25% (ABBA runs, profiles/ab/r06n_*).
+
 Launches of at most 16 frames run overlapped on extra streams (tuning key 9), and the contexts
 of every build after the first then share the process's hardware queues (GPU_MAX_HW_QUEUES=4)
 with the first's: measured 15-25% slower whichever build comes second.  Compare such launch
@@ -81,8 +84,12 @@ def main():
     if len(set(seg.values())) != 1:   # builds that change the image (timing experiments)
         print("segment counts differ between builds (each build's own count is used): %s" % seg)
     res = {l: [] for l in libs}
+    # the order rotates every round: the build timed first in a round measured about 0.25% slow
+    # (ABBA runs of identical settings, profiles/ab/r06n_*), so a fixed order biased every A/B
+    # by up to that much in favour of the later entries
     for rnd in range(a.rounds + 1):             # round 0 warms every build up
-        for l in libs:
+        k = rnd % len(libs)
+        for l in libs[k:] + libs[:k]:
             pt = pts[l]
             t0 = time.perf_counter()
             for f0 in range(1, a.spp + 1, a.chunk):
