@@ -223,11 +223,12 @@ def test_overlap_slots_grow_and_switch(cornell_scene, slots):
     assert_bitwise(got, want, "%d slots" % slots)
 
 
-@pytest.mark.parametrize("world,lag", [(1, 1), (1, 2), (3, 2)])
+@pytest.mark.parametrize("world,lag", [(1, 1), (1, 2), (3, 2), (1, 3)])
 def test_present_pipelined(cornell_scene, world, lag):
     """pt_present_begin / _end: the reference's show-every-frame loop with the readback of
     frame f-lag overlapping the renders of the later frames (lag + 1 pinned buffers in
-    rotation).  Every presented image equals the host ACES of the oracle's accumulation after
+    rotation; the copies run on their own stream from a ring of three device views, which lag 3
+    wraps while earlier copies may be in flight).  Every presented image equals the host ACES of the oracle's accumulation after
     that frame, byte for byte, for each row-split rank; a buffer begun twice holds the later
     image; misuse is refused."""
     W, Hh, n = 72, 40, 7
