@@ -1,8 +1,8 @@
 """The launch shapes bench.py times, in shading mode (display mode 1), against the oracle.
 
 bench.py's C2 step is one render of frames 1..1024 at 1920x1080 (one fused launch), C3 / C4
-one render of frames 1..256 (computeShader.c:505-554 per pixel and frame, the running mean of
-:548-551).  Those launches take branches that short test renders never reach:
+one render of frames 1..256, C5 frames 1..4096 at 3840x2160 as replays of a captured graph
+(computeShader.c:505-554 per pixel and frame, the running mean of :548-551).  Those launches take branches that short test renders never reach:
   * a fresh context's first long render runs a 2-frame probe launch, sorts the tile costs and
     then renders the rest as the continuation (pt_render.hip enqueue_frames);
   * frame-split work items of 16 frames (LDS scenes) or 4 (global-memory scenes), which only
@@ -99,3 +99,22 @@ def test_c3_c4_launch_256_frames_timed_size(scenes, name):
     first, second = _bench_like(sc, W, Hh, spp)
     assert_bitwise(first[ys, xs], want, "%s 256 frames 1080p, cold" % name)
     assert_bitwise(second[ys, xs], want, "%s 256 frames 1080p, warm" % name)
+
+
+def test_c5_graph_4096_frames_timed_shape(cornell_scene):
+    """C5's timed shape: 3840x2160, frames 1..4096 as two replays of a captured graph of 8
+    launches x 256 frames (the device frame counter crosses the seed's signed-overflow frame
+    2986 inside a launch), sampled pixels plus the first and last rows against the oracle."""
+    W, Hh, spp = 3840, 2160, 4096
+    pt = H.PathTracer(W, Hh, max_bounce=8)
+    pt.upload(cornell_scene)
+    pt.progressive_setup(frames_per_launch=256, launches_per_replay=8)
+    pt.progressive_reset(1)
+    pt.progressive_run(replays=spp // (256 * 8))
+    got = pt.read_rgba32f()
+    pt.close()
+    xs, ys = _sample(W, Hh, 600, 23)
+    keep = np.concatenate([np.arange(600), 600 + np.arange(0, 2 * W, 16)])   # every 16th pixel of the two rows
+    xs, ys = xs[keep], ys[keep]
+    want = O.render_pixels(cornell_scene, W, Hh, xs, ys, max_bounce=8, n_frames=spp)
+    assert_bitwise(got[ys, xs], want, "C5 4K 4096 frames through the graph")
