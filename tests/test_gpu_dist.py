@@ -54,9 +54,11 @@ def test_bench_ranks_gloo_one_gpu(tmp_path, cornell_scene, world, config):
         cmd += ["--traffic-json", tj]
     r = subprocess.run(cmd, cwd=REPO, env=env, capture_output=True, text=True, timeout=420)
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
+    import json
+    line = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
+    # rank 0 checks the assembled frame of the timed steps against the oracle
+    assert line["parity"]["mismatches"] == 0 and line["parity"]["words"] > 0, line["parity"]
     if tj:
-        import json
-        line = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
         rf = line["roofline"]
         assert rf["frac"] is not None and rf["bound"] == "valu" and "rank 0" in rf["share"], rf
     img = np.load(out)
