@@ -16,6 +16,13 @@ over the same frames (reference traversal semantics; identical image).
 The default run (C2 on one GPU) also times the global-memory configs C3 and C4 (2 steps each)
 and reports them under "secondary", each with its own roofline.
 
+Every line carries its own parity check (`parity`): after the timed region rank 0 renders
+sampled pixels of the timed image (frames 1..spp, the assembled frame at N > 1) with the CPU
+oracle (test infrastructure, never timed) and counts the words that differ; on one GPU the
+frames of the cpu_baseline sample are also re-rendered on the timed context and compared in
+full with the oracle image that leg computes.  --force-dist takes the N > 1 path (process
+group, scene broadcast, device row copy, all-gather) at world size 1.
+
 Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--config C2|C3|C4|C5]
 N>1:   python -m torch.distributed.run --nproc-per-node N bench.py --gpus N ...
 """
