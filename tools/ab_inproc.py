@@ -50,6 +50,7 @@ def main():
     ap.add_argument("--width", type=int, default=1920)
     ap.add_argument("--height", type=int, default=1080)
     ap.add_argument("--world", type=int, default=1, help="render rank 0 of a WORLD-way row split (per-GPU share)")
+    ap.add_argument("--rank", type=int, default=0, help="... or this rank of it")
     ap.add_argument("--key", action="append", default=[], help="pt_set_tuning key=value for every build (repeatable)")
     a = ap.parse_args()
     libs = a.libs.split(",")
@@ -69,7 +70,7 @@ def main():
     pts, seg = {}, {}
     for l in libs:
         H = hosts[l]
-        pt = H.PathTracer(a.width, a.height, max_bounce=8, rank=0, world=a.world)
+        pt = H.PathTracer(a.width, a.height, max_bounce=8, rank=a.rank, world=a.world)
         pt.upload(H.setupBuffers(obj, mtl))
         for kv in a.key + own_keys[l]:
             k, v = (int(x) for x in kv.split("="))

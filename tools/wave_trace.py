@@ -21,9 +21,10 @@ ap.add_argument("--reps", type=int, default=20)
 ap.add_argument("--scene", default="cornell")
 ap.add_argument("--width", type=int, default=1920)
 ap.add_argument("--height", type=int, default=1080)
+ap.add_argument("--world", type=int, default=1, help="rank 0 of a WORLD-way row split")
 a = ap.parse_args()
 sb = H.setupBuffers(*pt_scenes.write_scene(a.scene, os.path.join(REPO, "scenes")))
-pt = H.PathTracer(a.width, a.height, max_bounce=8)
+pt = H.PathTracer(a.width, a.height, max_bounce=8, rank=0, world=a.world)
 pt.upload(sb)
 pt.set_key(9, 1)
 fn = H.lib().pt_debug_wave_trace
@@ -33,14 +34,15 @@ N = 16384
 buf = np.zeros(4 * N, np.uint64)
 f = 1
 res = []
-for r in range(a.reps + 5):
+warm = 5 if a.frames <= 64 else 1
+for r in range(a.reps + warm):
     fn(buf, N, 1)
     pt.render(f, a.frames, 0 if f == 1 else 1)
     f += a.frames
     fn(buf, N, 0)
     t = buf.reshape(N, 4).astype(np.int64)
     t = t[t[:, 0] > 0]
-    if r < 5:
+    if r < warm:
         continue
     t0 = t[:, 0].min()
     entry, staged, end, items = (t[:, 0] - t0) * 10.0, (t[:, 1] - t0) * 10.0, (t[:, 2] - t0) * 10.0, t[:, 3]
