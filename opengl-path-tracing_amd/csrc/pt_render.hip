@@ -305,7 +305,11 @@ __device__ __forceinline__ void node_at(const SceneView& S, int i, float4& lo, f
 
 template <bool LDS>
 __device__ __forceinline__ float4 tri_quad(const SceneView& S, int slot, int k) {
+#ifdef PT_DIAG_TRIS_GLOBAL   // diagnostic build (LDS bank-conflict attribution): triangles from HBM
+    return S.tris[4 * slot + k];
+#else
     return LDS ? S.tris[slot + k * S.tp] : S.tris[4 * slot + k];
+#endif
 }
 
 __device__ __forceinline__ float qdiv(float a, float b, float rb) {
@@ -798,6 +802,13 @@ __global__ __launch_bounds__(NT, MINW) void k_render_sm(KParams p) {
         S.spheres = lds + nn + nt + nm;
         S.np = N;
         S.tp = T;
+#ifdef PT_DIAG_TRIS_GLOBAL
+        S.tris = p.sc.tris;
+#endif
+#ifdef PT_DIAG_SHADE_GLOBAL  // diagnostic build: materials and spheres from HBM
+        S.mats = p.sc.mats;
+        S.spheres = p.sc.spheres;
+#endif
         S.cm[0] = p.cons_m[0];
         S.cm[1] = p.cons_m[1];
         S.cm[2] = p.cons_m[2];
