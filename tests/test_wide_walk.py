@@ -152,3 +152,28 @@ def test_any_order_closest_hit(tmp_path, cornell_scene, ship_scene):
         assert res["mismatches_near_first"] == 0 and res["mismatches_static_order"] == 0, res
         assert res["uncertified_winners"] <= res["segments"] // 1000, res
         assert res["visits_near_first"] <= res["visits_reference"] * 1.02, res
+
+
+def test_k_wide_cut_visits(tmp_path, cornell_scene, ship_scene):
+    """K-wide trees cut from the reference's tree by the surface-area-optimal rule (K = 2, 4,
+    8; tests/wide/widek_sim.cpp), walked in preorder with children culled at the t of the
+    record visit: the reference's hits on every segment, and fewer record visits for wider
+    records but more child box tests from K = 4 to 8 -- the cost that sets the wide walk's pace
+    (on the C3 / C4 stand-ins +25% / +18% child tests for 36% / 40% fewer visits)."""
+    exe = str(tmp_path / "widek_sim")
+    subprocess.check_call(["g++", "-O2", "-std=c++17", "-ffp-contract=off", "-o", exe,
+                           os.path.join(REPO, "tests", "wide", "widek_sim.cpp")])
+    for name, sb, stride in (("cornell", cornell_scene, 11), ("ship", ship_scene, 17)):
+        path = str(tmp_path / ("%s.bin" % name))
+        with open(path, "wb") as f:
+            np.array([len(sb["tris"]), len(sb["nodes"]), len(sb["mats"]), len(sb["spheres"])], np.int32).tofile(f)
+            for k in ("tris", "nodes", "mats", "spheres", "cam"):
+                np.ascontiguousarray(sb[k], np.float32).tofile(f)
+        r = subprocess.run([exe, path, str(stride)], capture_output=True, text=True, timeout=600)
+        assert r.returncode == 0, r.stderr
+        res = json.loads(r.stdout.strip().splitlines()[-1])
+        assert res["segments"] > 4000, res
+        for k in ("K2", "K4", "K8"):
+            assert res[k]["mismatches"] == 0, (name, res)
+        assert res["K8"]["visits"] < res["K4"]["visits"] < res["K2"]["visits"], (name, res)
+        assert res["K8"]["records"] < res["K4"]["records"] < res["K2"]["records"], (name, res)
